@@ -1,0 +1,133 @@
+"""ctypes binding of libbo_amd.so (include/bo_amd.h).
+
+The product path has no CPU fallback: if the library or a HIP device is missing the
+calls raise ``BoNativeError`` / ``RuntimeError``.  Error statuses of the fit entry
+points map to ``numpy.linalg.LinAlgError`` exactly like the reference's LAPACK calls
+(bayesopt/numba_kernels.py:214, :401).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BO_AMD_LIB", os.path.join(_HERE, "libbo_amd.so"))
+
+MAX_OBJ = 8
+MAX_DIM = 8
+MAX_TOPQ = 48
+
+OK, ERR_ARG, ERR_UNSUPPORTED, ERR_WORKSPACE, ERR_HIP, ERR_NOT_PD, ERR_SINGULAR = range(7)
+CAND_I64, CAND_F64, CAND_GRID = 0, 1, 2
+
+c_dbl_p = C.POINTER(C.c_double)
+c_vp = C.c_void_p
+
+
+class BoNativeError(RuntimeError):
+    def __init__(self, status, what):
+        self.status = status
+        super().__init__(f"{what}: {status_string(status)} (status {status})")
+
+
+class PredictDesc(C.Structure):
+    """Mirror of bo_predict_desc (include/bo_amd.h)."""
+
+    _fields_ = [
+        ("n_obj", C.c_int32), ("dim", C.c_int32), ("n_train", C.c_int64),
+        ("x_train", c_vp), ("y_train", c_vp), ("ld_y", C.c_int64),
+        ("kinv", c_vp), ("ld_k", C.c_int64),
+        ("cand_kind", C.c_int32), ("reserved0", C.c_int32),
+        ("cand", c_vp), ("n_cand", C.c_int64), ("cand_offset", C.c_int64),
+        ("grid_lo", C.c_int64 * MAX_DIM), ("grid_shape", C.c_int64 * MAX_DIM),
+        ("excl_points", c_vp), ("n_excl", C.c_int64),
+        ("prior_mean", C.c_double * MAX_OBJ), ("prior_var", C.c_double * MAX_OBJ),
+        ("length_scale", C.c_double * MAX_OBJ), ("beta", C.c_double * MAX_OBJ),
+        ("mu", c_vp), ("var", c_vp), ("std_mu", c_vp), ("std_var", c_vp),
+        ("ucb", c_vp), ("acq", c_vp), ("ld_out", C.c_int64),
+        ("topq", C.c_int32), ("reserved1", C.c_int32),
+        ("top_val", c_vp), ("top_idx", c_vp),
+    ]
+
+
+_SIGS = {
+    "bo_abi_version": (C.c_int, []),
+    "bo_status_string": (C.c_char_p, [C.c_int]),
+    "bo_device_count": (C.c_int, []),
+    "bo_predict_workspace_size": (C.c_size_t, [C.POINTER(PredictDesc)]),
+    "bo_predict_acquire": (C.c_int, [C.POINTER(PredictDesc), c_vp, C.c_size_t, c_vp]),
+    "bo_update_k": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, C.c_int32, C.c_int64, C.c_int64,
+                              c_dbl_p, c_dbl_p, c_vp]),
+    "bo_update_k_star": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, C.c_int32, C.c_int32, c_vp,
+                                   C.c_int64, C.c_int64, C.c_int64, c_dbl_p, c_dbl_p, c_vp]),
+    "bo_update_mean_variance": (C.c_int, [c_vp, c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp,
+                                          C.c_int64, c_vp, C.c_int64, C.c_int64, c_dbl_p, c_dbl_p,
+                                          c_vp, C.c_size_t, c_vp]),
+    "bo_update_mean_variance_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
+    "bo_standardize_ucb_hvi": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C.c_int32, C.c_int64,
+                                         c_dbl_p, c_dbl_p, c_dbl_p, c_vp]),
+    "bo_select_topq": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, C.POINTER(C.c_int64),
+                                 C.POINTER(C.c_int64), C.c_int32, C.c_int64, c_vp, C.c_int64,
+                                 C.c_int32, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
+    "bo_select_topq_workspace_size": (C.c_size_t, [C.c_int64, C.c_int32]),
+    "bo_pareto_mask": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, c_vp]),
+    "bo_invert_k": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, C.c_size_t, c_vp]),
+    "bo_invert_k_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
+    "bo_compute_mll": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,
+                                 C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, c_vp, C.c_size_t,
+                                 c_vp]),
+    "bo_compute_mll_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
+    "bo_selftest_mfma_f64": (C.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "bo_profile_start": (C.c_int, [C.c_int]),
+    "bo_profile_stop": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libbo_amd.so and declare every exported symbol (raises if missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BoNativeError(ERR_UNSUPPORTED,
+                            f"{LIB_PATH} not built (run __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.bo_abi_version() != 1:
+        raise BoNativeError(ERR_UNSUPPORTED, "ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def symbols():
+    return list(_SIGS)
+
+
+def status_string(status):
+    try:
+        return load().bo_status_string(int(status)).decode()
+    except Exception:  # pragma: no cover - only used while formatting an error
+        return "unknown"
+
+
+def check(status, what):
+    if status == OK:
+        return
+    if status in (ERR_NOT_PD, ERR_SINGULAR):
+        raise np.linalg.LinAlgError(status_string(status))
+    raise BoNativeError(status, what)
+
+
+def dbl_array(values, n=None):
+    vals = [float(v) for v in values]
+    n = n or len(vals)
+    arr = (C.c_double * max(n, 1))(*vals)
+    return arr

@@ -1,0 +1,80 @@
+// Shared device helpers for the bo_amd kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bo_amd.h"
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+#define BO_CHECK_HIP(expr)                         \
+  do {                                             \
+    hipError_t _e = (expr);                        \
+    if (_e != hipSuccess) return BO_ERR_HIP;       \
+  } while (0)
+
+// MIN_VARIANCE / KERNEL_JITTER / CHOLESKY_JITTER: bayesopt/config.py:57-66 (fp64 branch).
+#define BO_MIN_VARIANCE 1e-10
+#define BO_KERNEL_JITTER 1e-6
+#define BO_CHOLESKY_JITTER 1e-8
+
+// ---------------------------------------------------------------------------------------
+// Selection order of select_next_batch (bayesopt/acquisition.py:134): the reference walks
+// np.argsort(acq)[::-1], so NaN comes first, then descending value.  Ties (unspecified
+// order in the reference) break by ascending global index.  Excluded / empty entries have
+// rank 0 and are never selected.
+// ---------------------------------------------------------------------------------------
+struct TopEntry {
+  double v;
+  long long i;  // global candidate index, -1 = empty/excluded
+};
+
+__device__ __forceinline__ int bo_rank(double v, long long i) {
+  return i < 0 ? 0 : (v != v ? 2 : 1);
+}
+
+// strict "a comes before b" in the selection order
+__device__ __forceinline__ bool bo_better(double av, long long ai, double bv, long long bi) {
+  const int ra = bo_rank(av, ai), rb = bo_rank(bv, bi);
+  if (ra != rb) return ra > rb;
+  if (ra == 1 && av != bv) return av > bv;
+  if (ra == 0) return false;
+  return ai < bi;
+}
+
+// Sort the 64 (v, i) pairs held one per lane into selection order (lane 0 best):
+// bitonic network over __shfl_xor (64-wide wavefront).
+__device__ __forceinline__ void bo_wave_sort64(double& v, long long& i) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const double pv = __shfl_xor(v, j, 64);
+      const long long pi = __shfl_xor(i, j, 64);
+      const bool lower = (lane & j) == 0;
+      const bool desc = (lane & k) == 0;
+      const bool take = (lower == desc) ? bo_better(pv, pi, v, i) : bo_better(v, i, pv, pi);
+      if (take) { v = pv; i = pi; }
+    }
+  }
+}
+
+// Merge up to 16 new entries (held by lanes 0..15 as nv/ni) into the wave's running
+// top-q list (lanes 0..q-1 hold it sorted; lanes >= q are empty).  q <= 48.
+__device__ __forceinline__ void bo_wave_topq_insert(double& lv, long long& li, double nv,
+                                                    long long ni, int q) {
+  const int lane = threadIdx.x & 63;
+  // threshold: does any new entry beat the current q-th entry?
+  const double tv = __shfl(lv, q - 1, 64);
+  const long long ti = __shfl(li, q - 1, 64);
+  const bool cand = lane < 16 && bo_better(nv, ni, tv, ti);
+  if (__ballot(cand) == 0ull) return;
+  const double sv = __shfl(nv, lane - 48, 64);
+  const long long si = __shfl(ni, lane - 48, 64);
+  if (lane >= 48) { lv = sv; li = si; }
+  bo_wave_sort64(lv, li);
+  if (lane >= q) { lv = -__builtin_inf(); li = -1; }
+}

@@ -1,0 +1,733 @@
+// Fused GP posterior + UCB / "hypervolume improvement" + top-q over a candidate shard.
+//
+// Replaces the reference chain bayesopt/bayesian_optimization.py:145-207:
+//   update_k_star (numba_kernels.py:406-442) -> update_mean (:450-488) ->
+//   update_variance (:491-535) -> standardize_objectives (:538-570) ->
+//   update_ucb / update_hypervolume_improvement (acquisition.py:55-108) ->
+//   select_next_batch (acquisition.py:116-144, local top-q part).
+//
+// MI355X design:
+//   * One wave owns 16 candidates.  For objective o it generates the K* column block
+//     K*[f][j] = pv_o * exp(-0.5 |x_f - c_j|^2 / ls_o^2) straight into the B-operand
+//     registers of v_mfma_f64_16x16x4_f64 (lane l: f = 4s + (l>>4), j = l & 15), so
+//     K* never touches LDS or HBM.
+//   * Z = K^-1 K* runs on the f64 matrix cores: the A operand (K^-1) is pre-packed in
+//     fragment order (one coalesced 16-B load per lane covers two k-steps) and streamed
+//     from L2 with a 4-deep register prefetch ring.
+//   * The quadratic form sum_e K*[e][j] Z[e][j] needs K* in the accumulator layout; for
+//     v_mfma_f64_16x16x4 the C rows (l>>4)+4r coincide with the B-fragment rows of k-step
+//     4E+r, so the epilogue selects them from registers (single-panel) or recomputes the
+//     4 exps (multi-panel, N > 512).
+//   * mu, var, standardisation, UCB and Sigma-UCB are computed in registers; the local
+//     top-q runs as a 64-lane bitonic network over shuffles with a ballot threshold.
+//   * Persistent grid (one 256-thread workgroup per CU, 1 wave per SIMD), tiles of 64
+//     candidates grid-strided; per-wave top-q lists merged by a second tiny kernel.
+
+#include "bo_common.h"
+
+#include <string.h>
+#include <math.h>
+
+#include <vector>
+
+namespace {
+
+constexpr int kWaves = 4;               // waves per workgroup
+constexpr int kTile = 16 * kWaves;      // candidates per workgroup tile
+constexpr int kPanelSteps = 128;        // k-steps of 4 training rows per register panel (512 rows)
+constexpr int kPF = 4;                  // prefetch depth (pairs of k-steps)
+
+struct FusedArgs {
+  int n_obj, dim, n_train, n_pad;       // n_pad = padded training rows (multiple of 32)
+  int n_panels;                          // register panels of 512 rows (multi-panel only)
+  int n_excl;
+  int cand_kind, topq;
+  long long n_cand, cand_offset, ld_out, n_tiles;
+  long long grid_lo[BO_MAX_DIM], grid_shape[BO_MAX_DIM];
+  const void* cand;
+  const double* xpad;                    // [n_pad][DIM] training rows, padded rows = 1e200
+  const double* excl;                    // [n_excl][DIM] evaluated points
+  const d2* wpack;                       // packed K^-1 (pack_kinv_kernel layout)
+  unsigned int wpack_bytes;
+  const double* alpha;                   // [n_obj][n_pad] = K^-1 (y - pm)
+  double pm[BO_MAX_OBJ], pv[BO_MAX_OBJ], nhl[BO_MAX_OBJ], beta[BO_MAX_OBJ], rsq_pv[BO_MAX_OBJ];
+  double *mu, *var, *std_mu, *std_var, *ucb, *acq;
+  TopEntry* partial;                     // [gridDim.x * kWaves][topq]
+  const double* kstar;                   // KMEM: materialised k_star [n_obj][ks_rows][n_cand]
+  long long ks_rows;
+};
+
+template <int DIM>
+__device__ __forceinline__ void load_candidate(const FusedArgs& a, long long j, bool valid,
+                                               double (&c)[DIM]) {
+#pragma unroll
+  for (int k = 0; k < DIM; ++k) c[k] = 0.0;
+  if (!valid) return;
+  if (a.cand_kind == BO_CAND_GRID) {
+    long long gi = a.cand_offset + j;
+#pragma unroll
+    for (int k = DIM - 1; k >= 0; --k) {
+      if (k < a.dim) {
+        const long long n = a.grid_shape[k];
+        const long long q = gi / n;
+        c[k] = (double)(a.grid_lo[k] + (gi - q * n));
+        gi = q;
+      }
+    }
+  } else if (a.cand_kind == BO_CAND_I64) {
+    const long long* p = (const long long*)a.cand + j * a.dim;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k)
+      if (k < a.dim) c[k] = (double)p[k];
+  } else {
+    const double* p = (const double*)a.cand + j * a.dim;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k)
+      if (k < a.dim) c[k] = p[k];
+  }
+}
+
+// squared distance between LDS row `row` ([*][DIM], 16-B aligned) and the candidate;
+// numba_kernels.py:436-437 (diff = x_e - c_i, then diff . diff)
+template <int DIM>
+__device__ __forceinline__ double sqdist(const double* xs, int row, const double (&c)[DIM]) {
+  const d2* r = (const d2*)(xs + row * DIM);
+  double sq = 0.0;
+#pragma unroll
+  for (int k = 0; k < DIM / 2; ++k) {
+    const d2 x = r[k];
+    const double d0 = x.x - c[2 * k], d1 = x.y - c[2 * k + 1];
+    sq = __builtin_fma(d0, d0, sq);
+    sq = __builtin_fma(d1, d1, sq);
+  }
+  return sq;
+}
+
+__device__ __forceinline__ double kstar_at(const FusedArgs& a, int o, int f, long long j, bool valid) {
+  return (valid && f < a.n_train) ? a.kstar[((long long)o * a.ks_rows + f) * a.n_cand + j] : 0.0;
+}
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// One panel's contraction for E-blocks (2*ep, 2*ep+1): acc0/acc1 += W[E, panel] . B.
+// The packed stream of a panel is ordered (ep, pair, which, lane): every load is one
+// contiguous 1 KiB wave-row at scalar offset `base + ((ep*NPAIR + pair)*2 + which) KiB`.
+// The prefetch ring (kPF pairs deep) carries across ep boundaries; the caller primes it.
+template <int NS, bool SELECT>
+__device__ __forceinline__ void panel_epair(__amdgpu_buffer_rsrc_t wr, int voff, int base,
+                                            int ep, const double (&B)[NS],
+                                            d2 (&wa)[kPF], d2 (&wb)[kPF], d4& acc0, d4& acc1,
+                                            double (&sel0)[4], double (&sel1)[4]) {
+  constexpr int NPAIR = NS / 2;
+  const int so0 = base + ((ep * NPAIR * 2) << 10);
+#pragma unroll
+  for (int p = 0; p < NPAIR; ++p) {
+    const d2 ca = wa[p % kPF];
+    const d2 cb = wb[p % kPF];
+    // prefetch kPF pairs ahead; past the end of the stream the buffer range check
+    // returns zeros (no fault), so the load needs no condition
+    wa[p % kPF] = wload(wr, voff, so0 + (((p + kPF) * 2) << 10));
+    wb[p % kPF] = wload(wr, voff, so0 + (((p + kPF) * 2 + 1) << 10));
+    acc0 = mfma64(ca.x, B[2 * p], acc0);
+    acc1 = mfma64(cb.x, B[2 * p], acc1);
+    acc0 = mfma64(ca.y, B[2 * p + 1], acc0);
+    acc1 = mfma64(cb.y, B[2 * p + 1], acc1);
+    if (SELECT && (p & 1) == 1) {
+      const int c = p >> 1;  // chunk of 4 k-steps = rows 16c..16c+15
+      const double m0 = (c == 2 * ep) ? 1.0 : 0.0, m1 = (c == 2 * ep + 1) ? 1.0 : 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sel0[r] = __builtin_fma(m0, B[4 * c + r], sel0[r]);
+        sel1[r] = __builtin_fma(m1, B[4 * c + r], sel1[r]);
+      }
+    }
+  }
+}
+
+template <int NS>
+__device__ __forceinline__ void prime_ring(__amdgpu_buffer_rsrc_t wr, int voff, int base,
+                                           d2 (&wa)[kPF], d2 (&wb)[kPF]) {
+#pragma unroll
+  for (int p = 0; p < kPF; ++p) {
+    if (p < NS / 2) {
+      wa[p] = wload(wr, voff, base + ((2 * p) << 10));
+      wb[p] = wload(wr, voff, base + ((2 * p + 1) << 10));
+    }
+  }
+}
+
+// NS = k-steps held in registers per panel (NS*4 training rows); DIM = padded input
+// dimension (2, 4 or 8; padded coordinates are 0 on both sides); MULTI = several panels.
+template <int NS, int DIM, bool MULTI, bool KMEM>
+__global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* xs = smem;                                   // [n_pad][DIM] training rows
+  double* alpha = xs + (size_t)a.n_pad * DIM;          // [n_obj][n_pad]
+  double* exs_buf = alpha + (size_t)a.n_obj * a.n_pad; // [n_excl][DIM] (separate set only)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, jl = lane & 15;
+
+  for (int t = tid; t < a.n_pad * DIM; t += blockDim.x) xs[t] = a.xpad[t];
+  for (int t = tid; t < a.n_obj * a.n_pad; t += blockDim.x) alpha[t] = a.alpha[t];
+  const double* exs = a.excl ? exs_buf : xs;   // NULL: the evaluated points are x_train
+  if (a.excl)
+    for (int t = tid; t < a.n_excl * DIM; t += blockDim.x) exs_buf[t] = a.excl[t];
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
+  const int voff = lane * 16;
+
+  double top_v = -__builtin_inf();
+  long long top_i = -1;
+  const int n_ep = a.n_pad / 32;                           // E-block pairs over all rows
+  const int w_obj = a.n_pad * a.n_pad * 8;                 // bytes per objective
+  const int w_panel = a.n_pad * (NS * 4) * 8;              // bytes per panel
+
+  for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const long long j = tile * kTile + wave * 16 + jl;
+    const bool valid = j < a.n_cand;
+    double c[DIM];
+    if (!KMEM) load_candidate<DIM>(a, j, valid, c);
+    else {
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) c[k] = 0.0;
+    }
+
+    // exclusion (acquisition.py:137-139): candidate equal, coordinate by coordinate, to an
+    // evaluated point.  Lane group g checks points g, g+4, ...
+    bool hit = false;
+    for (int e = g; e < (KMEM ? 0 : a.n_excl); e += 4) {
+      const d2* r = (const d2*)(exs + e * DIM);
+      bool eq = true;
+#pragma unroll
+      for (int k = 0; k < DIM / 2; ++k) {
+        const d2 x = r[k];
+        eq = eq && (x.x == c[2 * k]) && (x.y == c[2 * k + 1]);
+      }
+      hit = hit || eq;
+    }
+    const unsigned long long hb = __ballot(hit);
+    const bool excluded =
+        ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
+
+    double acq = 0.0;
+    for (int o = 0; o < a.n_obj; ++o) {
+      const double pv = a.pv[o], nhl = a.nhl[o];
+      const double* al = alpha + o * a.n_pad;
+      double qpart = 0.0, mpart = 0.0;
+      for (int panel = 0; panel < (MULTI ? a.n_panels : 1); ++panel) {
+        const int f0 = panel * NS * 4;
+        // K* block for this lane: B[s] = K*[f0 + 4s + g][j]  (numba_kernels.py:440-442);
+        // padded rows sit at 1e200 so their exp underflows to exactly 0.
+        double B[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const int f = f0 + 4 * s + g;
+          if (KMEM) B[s] = kstar_at(a, o, f, j, valid);
+          else B[s] = pv * exp(sqdist<DIM>(xs, f, c) * nhl);
+          if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        const int base = o * w_obj + panel * w_panel;
+        d2 wa[kPF], wb[kPF];
+        prime_ring<NS>(wr, voff, base, wa, wb);
+        for (int ep = 0; ep < n_ep; ++ep) {
+          d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+          double sel0[4] = {0.0, 0.0, 0.0, 0.0}, sel1[4] = {0.0, 0.0, 0.0, 0.0};
+          panel_epair<NS, !MULTI>(wr, voff, base, ep, B, wa, wb, acc0, acc1, sel0, sel1);
+          if (MULTI) {
+            // recompute K*[e][j] for the accumulator rows e = 16E + g + 4r
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int e0 = 32 * ep + g + 4 * r, e1 = e0 + 16;
+              if (KMEM) {
+                sel0[r] = kstar_at(a, o, e0, j, valid);
+                sel1[r] = kstar_at(a, o, e1, j, valid);
+              } else {
+                sel0[r] = pv * exp(sqdist<DIM>(xs, e0, c) * nhl);
+                sel1[r] = pv * exp(sqdist<DIM>(xs, e1, c) * nhl);
+              }
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            qpart = __builtin_fma(sel0[r], acc0[r], qpart);
+            qpart = __builtin_fma(sel1[r], acc1[r], qpart);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) mpart = __builtin_fma(al[f0 + 4 * s + g], B[s], mpart);
+      }
+      // reduce over the 4 lane groups holding the same candidate
+      qpart += __shfl_xor(qpart, 16, 64);
+      qpart += __shfl_xor(qpart, 32, 64);
+      mpart += __shfl_xor(mpart, 16, 64);
+      mpart += __shfl_xor(mpart, 32, 64);
+
+      const double pm = a.pm[o];
+      const double mu = pm + mpart;                                   // :486-488
+      const double var = fmax(pv - qpart, BO_MIN_VARIANCE);           // :532-535
+      const double smu = (mu - pm) / a.rsq_pv[o];                      // :563-565
+      const double svar = var / pv;                                    // :568-570
+      const double u = smu + a.beta[o] * sqrt(fabs(svar));             // acquisition.py:52
+      acq = (o == 0) ? u : acq + u;                                    // acquisition.py:108
+      if (valid && g == 0) {
+        const long long off = (long long)o * a.ld_out + j;
+        if (a.mu) a.mu[off] = mu;
+        if (a.var) a.var[off] = var;
+        if (a.std_mu) a.std_mu[off] = smu;
+        if (a.std_var) a.std_var[off] = svar;
+        if (a.ucb) a.ucb[off] = u;
+      }
+    }
+    if (valid && g == 0 && a.acq) a.acq[j] = acq;
+    if (a.topq > 0) {
+      const long long gi = (valid && !excluded) ? a.cand_offset + j : -1;
+      bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+    }
+  }
+  if (a.topq > 0 && lane < a.topq) {
+    TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
+    dst[lane].v = top_v;
+    dst[lane].i = top_i;
+  }
+}
+
+// Training rows / evaluated points padded to [rows_pad][DIM]: coordinates beyond `dim`
+// are 0; rows beyond `rows` are `fill` (1e200 puts padded training rows at infinite
+// distance so exp() underflows to exactly 0).
+__global__ void pad_points_kernel(double* __restrict__ out, const double* __restrict__ in,
+                                  int rows, int rows_pad, int dim, int DIM, double fill) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows_pad * DIM) return;
+  const int r = t / DIM, k = t - r * DIM;
+  out[t] = r < rows ? (k < dim ? in[r * dim + k] : 0.0) : fill;
+}
+
+// Pack K^-1 (row-major, leading dim ld) into MFMA A-fragment order, zero padded:
+// out[o][panel][ep][pair][which][lane] (d2) = (W[16E + (l&15)][4s + (l>>4)], same at s+1),
+// E = 2ep + which, s = panel*NS + 2*pair (global k-step).
+__global__ void pack_kinv_kernel(d2* __restrict__ out, const double* __restrict__ kinv,
+                                 long long ld, int n, int n_pad, int ns_panel, int n_obj) {
+  const long long per_obj = (long long)n_pad * n_pad / 2;
+  const long long total = per_obj * n_obj;
+  const int n_ep = n_pad / 32;
+  const int npair = ns_panel / 2;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(t / per_obj);
+    long long r = t - (long long)o * per_obj;
+    const int lane = (int)(r & 63); r >>= 6;
+    const int which = (int)(r & 1); r >>= 1;
+    const int pair = (int)(r % npair); r /= npair;
+    const int ep = (int)(r % n_ep); r /= n_ep;
+    const int panel = (int)r;
+    const int row = 16 * (2 * ep + which) + (lane & 15);
+    const int s = panel * ns_panel + 2 * pair;
+    const int col0 = 4 * s + (lane >> 4), col1 = col0 + 4;
+    const double* wo = kinv + (long long)o * ld * ld;
+    d2 v;
+    v.x = (row < n && col0 < n) ? wo[(long long)row * ld + col0] : 0.0;
+    v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
+    out[t] = v;
+  }
+}
+
+// alpha[o][f] = sum_e Kinv[o][f][e] * (y[e][o] - pm[o])   (numba_kernels.py:477-483),
+// e ascending, zero for padded rows.  One wave per row: lane-strided partial sums then
+// a shuffle tree (order differs from BLAS dgemv only in the last bits).
+__global__ void alpha_kernel(double* __restrict__ alpha, const double* __restrict__ kinv,
+                             long long ld, const double* __restrict__ y, long long ld_y, int n,
+                             int n_pad, int n_obj, FusedArgs a) {
+  const int lane = threadIdx.x & 63;
+  const long long row_id = blockIdx.x * (long long)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row_id >= (long long)n_obj * n_pad) return;
+  const int o = (int)(row_id / n_pad), f = (int)(row_id % n_pad);
+  double s = 0.0;
+  if (f < n) {
+    const double* wr = kinv + (long long)o * ld * ld + (long long)f * ld;
+    const double pm = a.pm[o];
+    for (int e = lane; e < n; e += 64) s = __builtin_fma(wr[e], y[(long long)e * ld_y + o] - pm, s);
+  }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (lane == 0) alpha[row_id] = s;
+}
+
+// Merge the per-wave lists [n_lists][q] into the final top-q (one workgroup, 16 waves).
+__global__ __launch_bounds__(1024) void topq_merge_kernel(const TopEntry* __restrict__ lists,
+                                                          int n_lists, int q,
+                                                          double* __restrict__ out_v,
+                                                          long long* __restrict__ out_i) {
+  __shared__ TopEntry stage[16 * BO_MAX_TOPQ];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  double lv = -__builtin_inf();
+  long long li = -1;
+  const long long total = (long long)n_lists * q;
+  for (long long base = (long long)wave * 16; base < total; base += (long long)nw * 16) {
+    double nv = -__builtin_inf();
+    long long ni = -1;
+    if (lane < 16 && base + lane < total) { nv = lists[base + lane].v; ni = lists[base + lane].i; }
+    bo_wave_topq_insert(lv, li, nv, ni, q);
+  }
+  if (lane < q) { stage[wave * q + lane].v = lv; stage[wave * q + lane].i = li; }
+  __syncthreads();
+  if (wave == 0) {
+    double fv = -__builtin_inf();
+    long long fi = -1;
+    for (int base = 0; base < nw * q; base += 16) {
+      double nv = -__builtin_inf();
+      long long ni = -1;
+      if (lane < 16 && base + lane < nw * q) { nv = stage[base + lane].v; ni = stage[base + lane].i; }
+      bo_wave_topq_insert(fv, fi, nv, ni, q);
+    }
+    if (lane < q) { out_v[lane] = fv; out_i[lane] = fi; }
+  }
+}
+
+__global__ void selftest_mfma_kernel(const double* a, const double* b, double* d) {
+  const int l = threadIdx.x;
+  const double av = a[(l & 15) * 4 + (l >> 4)];  // A[i=l&15][k=l>>4]
+  const double bv = b[(l >> 4) * 16 + (l & 15)]; // B[k=l>>4][j=l&15]
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  acc = mfma64(av, bv, acc);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) d[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
+}
+
+inline int pad_rows(long long n) { return (int)((n + 31) / 32 * 32); }
+inline int pad_dim(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : (d <= 6 ? 6 : 8)); }
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Plan {
+  int n_pad, ns, n_panels, dim_pad, n_excl;
+  bool multi;
+  size_t off_alpha, off_xpad, off_excl, off_partial, total;
+  int grid;
+  size_t lds;
+};
+
+int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
+    cus = p.multiProcessorCount;
+  }
+  return cus;
+}
+
+int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device) {
+  if (!d || d->n_obj < 1 || d->n_obj > BO_MAX_OBJ || d->dim < 1 || d->dim > BO_MAX_DIM)
+    return BO_ERR_ARG;
+  if (d->n_train < 1 || d->n_cand < 0 || d->topq < 0 || d->topq > BO_MAX_TOPQ) return BO_ERR_ARG;
+  if (d->cand_kind < 0 || d->cand_kind > 2) return BO_ERR_ARG;
+  if (d->excl_points && d->n_excl < 0) return BO_ERR_ARG;
+  const long long n = d->n_train;
+  if (n > (1 << 14)) return BO_ERR_UNSUPPORTED;
+  int n_pad = pad_rows(n);
+  int ns;
+  bool multi = false;
+  if (n_pad <= 32) ns = 8;
+  else if (n_pad <= 64) ns = 16;
+  else if (n_pad <= 128) ns = 32;
+  else if (n_pad <= 256) ns = 64;
+  else if (n_pad <= 384) ns = 96;
+  else if (n_pad <= 512) ns = 128;
+  else { ns = kPanelSteps; multi = true; }
+  n_pad = multi ? (int)((n + 511) / 512 * 512) : ns * 4;
+  pl->n_pad = n_pad;
+  pl->ns = ns;
+  pl->multi = multi;
+  pl->n_panels = multi ? n_pad / 512 : 1;
+  pl->dim_pad = pad_dim(d->dim);
+  pl->n_excl = (int)(d->excl_points ? d->n_excl : n);
+  pl->lds = ((size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad +
+             (d->excl_points ? (size_t)pl->n_excl * pl->dim_pad : 0)) * sizeof(double);
+  if (pl->lds > 160 * 1024) return BO_ERR_UNSUPPORTED;
+  const size_t w_bytes = (size_t)d->n_obj * n_pad * n_pad * sizeof(double);
+  if (w_bytes >= (1ull << 31)) return BO_ERR_UNSUPPORTED;
+  const long long n_tiles = (d->n_cand + kTile - 1) / kTile;
+  const int cus = query_device ? num_cus() : 256;
+  pl->grid = (int)(n_tiles < cus ? (n_tiles > 0 ? n_tiles : 1) : cus);
+  pl->off_alpha = align256(w_bytes);
+  pl->off_xpad = pl->off_alpha + align256((size_t)d->n_obj * n_pad * sizeof(double));
+  pl->off_excl = pl->off_xpad + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
+  pl->off_partial = pl->off_excl + align256((size_t)(pl->n_excl + 1) * pl->dim_pad * sizeof(double));
+  // partial lists sized for the largest persistent grid any device could use
+  pl->total = pl->off_partial +
+              align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry)) + 256;
+  return BO_OK;
+}
+
+template <int NS, int DIM, bool MULTI, bool KMEM = false>
+hipError_t launch_fused(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) {
+  auto k = fused_predict_kernel<NS, DIM, MULTI, KMEM>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, fa);
+  return hipGetLastError();
+}
+
+// Optional timing of the fused kernel itself (bench.py's roofline): when enabled, every
+// fused launch is bracketed by a pair of HIP events on its stream.
+struct KernelTimer {
+  bool on = false;
+  int used = 0;
+  std::vector<hipEvent_t> ev;
+} g_timer;
+
+void timer_mark(hipStream_t s) {
+  if (!g_timer.on || g_timer.used >= (int)g_timer.ev.size()) return;
+  hipEventRecord(g_timer.ev[g_timer.used++], s);
+}
+
+template <int DIM>
+hipError_t launch_ns(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
+  if (pl.multi) return launch_fused<kPanelSteps, DIM, true>(fa, pl.grid, pl.lds, s);
+  switch (pl.ns) {
+    case 8: return launch_fused<8, DIM, false>(fa, pl.grid, pl.lds, s);
+    case 16: return launch_fused<16, DIM, false>(fa, pl.grid, pl.lds, s);
+    case 32: return launch_fused<32, DIM, false>(fa, pl.grid, pl.lds, s);
+    case 64: return launch_fused<64, DIM, false>(fa, pl.grid, pl.lds, s);
+    case 96: return launch_fused<96, DIM, false>(fa, pl.grid, pl.lds, s);
+    default: return launch_fused<128, DIM, false>(fa, pl.grid, pl.lds, s);
+  }
+}
+
+hipError_t launch_kmem(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
+  if (pl.multi) return launch_fused<kPanelSteps, 2, true, true>(fa, pl.grid, pl.lds, s);
+  switch (pl.ns) {
+    case 8: return launch_fused<8, 2, false, true>(fa, pl.grid, pl.lds, s);
+    case 16: return launch_fused<16, 2, false, true>(fa, pl.grid, pl.lds, s);
+    case 32: return launch_fused<32, 2, false, true>(fa, pl.grid, pl.lds, s);
+    case 64: return launch_fused<64, 2, false, true>(fa, pl.grid, pl.lds, s);
+    case 96: return launch_fused<96, 2, false, true>(fa, pl.grid, pl.lds, s);
+    default: return launch_fused<128, 2, false, true>(fa, pl.grid, pl.lds, s);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t bo_predict_workspace_size(const bo_predict_desc* d) {
+  Plan pl;
+  if (make_plan(d, &pl, false) != BO_OK) return 0;
+  return pl.total;
+}
+
+static int predict_impl(const bo_predict_desc* d, const double* kstar, long long ks_rows,
+                        void* workspace, size_t ws_bytes, void* stream) {
+  const bool kmem = kstar != nullptr;
+  Plan pl;
+  int st = make_plan(d, &pl, true);
+  if (st != BO_OK) return st;
+  if (!workspace || ws_bytes < pl.total) return BO_ERR_WORKSPACE;
+  if ((!kmem && !d->x_train) || !d->y_train || !d->kinv || d->ld_k < d->n_train ||
+      d->ld_y < d->n_obj)
+    return BO_ERR_ARG;
+  if (d->cand_kind != BO_CAND_GRID && d->n_cand > 0 && !d->cand) return BO_ERR_ARG;
+  if (d->topq > 0 && (!d->top_val || !d->top_idx)) return BO_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+
+  char* ws = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  d2* wpack = (d2*)ws;
+  double* alpha = (double*)(ws + pl.off_alpha);
+  double* xpad = (double*)(ws + pl.off_xpad);
+  double* excl = (double*)(ws + pl.off_excl);
+  TopEntry* partial = (TopEntry*)(ws + pl.off_partial);
+
+  FusedArgs fa;
+  memset(&fa, 0, sizeof(fa));
+  fa.n_obj = d->n_obj;
+  fa.dim = d->dim;
+  fa.n_train = (int)d->n_train;
+  fa.n_pad = pl.n_pad;
+  fa.n_panels = pl.n_panels;
+  fa.n_excl = pl.n_excl;
+  fa.cand_kind = d->cand_kind;
+  fa.topq = d->topq;
+  fa.n_cand = d->n_cand;
+  fa.cand_offset = d->cand_offset;
+  fa.ld_out = d->ld_out > 0 ? d->ld_out : d->n_cand;
+  fa.n_tiles = (d->n_cand + kTile - 1) / kTile;
+  for (int k = 0; k < BO_MAX_DIM; ++k) {
+    fa.grid_lo[k] = d->grid_lo[k];
+    fa.grid_shape[k] = d->grid_shape[k] > 0 ? d->grid_shape[k] : 1;
+  }
+  if (d->cand_kind == BO_CAND_GRID) {
+    long long total = 1;
+    for (int k = 0; k < d->dim; ++k) {
+      if (d->grid_shape[k] <= 0) return BO_ERR_ARG;
+      total *= d->grid_shape[k];
+    }
+    if (d->cand_offset < 0 || d->cand_offset + d->n_cand > total) return BO_ERR_ARG;
+  }
+  fa.cand = d->cand;
+  fa.xpad = xpad;
+  fa.excl = d->excl_points ? excl : nullptr;
+  fa.wpack = wpack;
+  fa.wpack_bytes = (unsigned int)((size_t)d->n_obj * pl.n_pad * pl.n_pad * sizeof(double));
+  fa.alpha = alpha;
+  for (int o = 0; o < d->n_obj; ++o) {
+    fa.pm[o] = d->prior_mean[o];
+    fa.pv[o] = d->prior_var[o];
+    const double ls = d->length_scale[o];
+    fa.nhl[o] = -0.5 / (ls * ls);
+    fa.beta[o] = d->beta[o];
+    fa.rsq_pv[o] = sqrt(d->prior_var[o]);
+  }
+  fa.mu = d->mu;
+  fa.var = d->var;
+  fa.std_mu = d->std_mu;
+  fa.std_var = d->std_var;
+  fa.ucb = d->ucb;
+  fa.acq = d->acq;
+  fa.partial = partial;
+  fa.kstar = kstar;
+  fa.ks_rows = ks_rows;
+
+  {
+    const long long total = (long long)d->n_obj * pl.n_pad * pl.n_pad / 2;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(pack_kinv_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k,
+                       (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
+    BO_CHECK_HIP(hipGetLastError());
+    const long long rows = (long long)d->n_obj * pl.n_pad;
+    hipLaunchKernelGGL(alpha_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, alpha,
+                       d->kinv, d->ld_k, d->y_train, d->ld_y, (int)d->n_train, pl.n_pad,
+                       d->n_obj, fa);
+    BO_CHECK_HIP(hipGetLastError());
+    int cnt = kmem ? 0 : pl.n_pad * pl.dim_pad;
+    if (cnt > 0) hipLaunchKernelGGL(pad_points_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, xpad,
+                       d->x_train, (int)d->n_train, pl.n_pad, d->dim, pl.dim_pad, 1e200);
+    BO_CHECK_HIP(hipGetLastError());
+    cnt = (kmem || !d->excl_points) ? 0 : pl.n_excl * pl.dim_pad;
+    if (cnt > 0) {
+      hipLaunchKernelGGL(pad_points_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, excl,
+                         d->excl_points ? d->excl_points : d->x_train, pl.n_excl, pl.n_excl,
+                         d->dim, pl.dim_pad, 0.0);
+      BO_CHECK_HIP(hipGetLastError());
+    }
+  }
+  if (d->n_cand == 0) {
+    if (d->topq > 0) {
+      BO_CHECK_HIP(hipMemsetAsync(d->top_idx, 0xff, sizeof(int64_t) * d->topq, s));
+    }
+    return BO_OK;
+  }
+  hipError_t e;
+  const bool timed = g_timer.on && g_timer.used + 2 <= (int)g_timer.ev.size();
+  if (timed) timer_mark(s);
+  if (kmem) e = launch_kmem(pl, fa, s);
+  else switch (pl.dim_pad) {
+    case 2: e = launch_ns<2>(pl, fa, s); break;
+    case 4: e = launch_ns<4>(pl, fa, s); break;
+    case 6: e = launch_ns<6>(pl, fa, s); break;
+    default: e = launch_ns<8>(pl, fa, s); break;
+  }
+  if (e != hipSuccess) return BO_ERR_HIP;
+  if (timed) timer_mark(s);
+  if (d->topq > 0) {
+    hipLaunchKernelGGL(topq_merge_kernel, dim3(1), dim3(1024), 0, s, partial, pl.grid * kWaves,
+                       d->topq, d->top_val, (long long*)d->top_idx);
+    BO_CHECK_HIP(hipGetLastError());
+  }
+  return BO_OK;
+}
+
+int bo_predict_acquire(const bo_predict_desc* d, void* workspace, size_t ws_bytes, void* stream) {
+  return predict_impl(d, nullptr, 0, workspace, ws_bytes, stream);
+}
+
+static void fill_mv_desc(bo_predict_desc* d, int32_t n_obj, int64_t n_cand, int64_t n) {
+  memset(d, 0, sizeof(*d));
+  d->n_obj = n_obj;
+  d->dim = 1;
+  d->n_train = n;
+  d->cand_kind = BO_CAND_GRID;
+  d->n_cand = n_cand;
+  d->grid_shape[0] = n_cand > 0 ? n_cand : 1;
+  d->n_excl = 0;
+}
+
+size_t bo_update_mean_variance_workspace_size(int32_t n_obj, int64_t current_eval) {
+  bo_predict_desc d;
+  fill_mv_desc(&d, n_obj, 0, current_eval);
+  d.excl_points = (const double*)1;  // no exclusion set
+  return bo_predict_workspace_size(&d);
+}
+
+int bo_update_mean_variance(double* mu, double* var, const double* k_star, int64_t ld_rows,
+                            int32_t n_obj, int64_t n_cand, const double* kinv, int64_t ld_k,
+                            const double* y, int64_t ld_y, int64_t current_eval,
+                            const double* prior_mean, const double* prior_variance,
+                            void* workspace, size_t workspace_bytes, void* stream) {
+  if (!k_star || ld_rows < current_eval || !prior_mean || !prior_variance) return BO_ERR_ARG;
+  if (n_obj < 1 || n_obj > BO_MAX_OBJ) return BO_ERR_ARG;
+  bo_predict_desc d;
+  fill_mv_desc(&d, n_obj, n_cand, current_eval);
+  d.excl_points = (const double*)1;
+  d.y_train = y;
+  d.ld_y = ld_y;
+  d.kinv = kinv;
+  d.ld_k = ld_k;
+  for (int o = 0; o < n_obj; ++o) {
+    d.prior_mean[o] = prior_mean[o];
+    d.prior_var[o] = prior_variance[o];
+    d.length_scale[o] = 1.0;
+    d.beta[o] = 0.0;
+  }
+  d.mu = mu;
+  d.var = var;
+  d.ld_out = n_cand;
+  return predict_impl(&d, k_star, ld_rows, workspace, workspace_bytes, stream);
+}
+
+int bo_profile_start(int max_launches) {
+  if (max_launches < 1) return BO_ERR_ARG;
+  for (auto& e : g_timer.ev) hipEventDestroy(e);
+  g_timer.ev.assign(2 * (size_t)max_launches, nullptr);
+  for (auto& e : g_timer.ev) BO_CHECK_HIP(hipEventCreate(&e));
+  g_timer.used = 0;
+  g_timer.on = true;
+  return BO_OK;
+}
+
+int bo_profile_stop(double* total_ms, int* launches) {
+  g_timer.on = false;
+  double tot = 0.0;
+  const int n = g_timer.used / 2;
+  for (int i = 0; i < n; ++i) {
+    BO_CHECK_HIP(hipEventSynchronize(g_timer.ev[2 * i + 1]));
+    float ms = 0.f;
+    BO_CHECK_HIP(hipEventElapsedTime(&ms, g_timer.ev[2 * i], g_timer.ev[2 * i + 1]));
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = n;
+  g_timer.used = 0;
+  return BO_OK;
+}
+
+int bo_selftest_mfma_f64(const double* a, const double* b, double* dd, void* stream) {
+  if (!a || !b || !dd) return BO_ERR_ARG;
+  hipLaunchKernelGGL(selftest_mfma_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, dd);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,334 @@
+// Elementwise / selection / Pareto kernels of the drop-in ABI:
+//   bo_update_k            numba_kernels.py:329-367  (RBF Gram)
+//   bo_update_k_star       numba_kernels.py:406-442  (materialised K*, unfused API)
+//   bo_standardize_ucb_hvi numba_kernels.py:538-570 + acquisition.py:55-108
+//   bo_select_topq         acquisition.py:116-144
+//   bo_pareto_mask         pareto.py:12-45
+// These are HBM-bound integer/compare/elementwise kernels: coalesced, one pass.
+
+#include "bo_common.h"
+
+#include <math.h>
+#include <string.h>
+
+namespace {
+
+struct HostParams {
+  double a[BO_MAX_OBJ], b[BO_MAX_OBJ], c[BO_MAX_OBJ];
+};
+
+// ----------------------------------------------------------------------------- Gram
+// One thread per (i, j>=i) pair of rows [last, cur): K[o][i][j] = K[o][j][i].
+__global__ void gram_kernel(double* __restrict__ km, long long ld, int n_obj,
+                            const double* __restrict__ x, int dim, int last, int cur,
+                            HostParams p) {
+  const int i = last + blockIdx.y;
+  const int j = i + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cur || j >= cur) return;
+  double sq = 0.0;
+  for (int k = 0; k < dim; ++k) {
+    const double d = x[(long long)i * dim + k] - x[(long long)j * dim + k];
+    sq = __builtin_fma(d, d, sq);
+  }
+  for (int o = 0; o < n_obj; ++o) {
+    // pv * exp(-0.5 * sq / ls^2)  (numba_kernels.py:358-360); p.b = ls^2
+    const double v = p.a[o] * exp(-0.5 * sq / p.b[o]);
+    double* ko = km + (long long)o * ld * ld;
+    ko[(long long)i * ld + j] = v;
+    ko[(long long)j * ld + i] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------ K*
+__global__ void kstar_kernel(double* __restrict__ ks, long long ld_rows, int n_obj,
+                             const double* __restrict__ x, int dim, int kind,
+                             const void* __restrict__ cand, long long n_cand, int last, int cur,
+                             HostParams p) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const int e = last + blockIdx.y;
+  if (i >= n_cand || e >= cur) return;
+  double sq = 0.0;
+  for (int k = 0; k < dim; ++k) {
+    const double c = kind == BO_CAND_I64 ? (double)((const long long*)cand)[i * dim + k]
+                                         : ((const double*)cand)[i * dim + k];
+    const double d = x[(long long)e * dim + k] - c;
+    sq = __builtin_fma(d, d, sq);
+  }
+  for (int o = 0; o < n_obj; ++o)
+    ks[((long long)o * ld_rows + e) * n_cand + i] = p.a[o] * exp(-0.5 * sq / p.b[o]);
+}
+
+// --------------------------------------------------------------- standardise/UCB/HVI
+__global__ void std_ucb_hvi_kernel(double* __restrict__ smu, double* __restrict__ svar,
+                                   double* __restrict__ ucb, double* __restrict__ acq,
+                                   const double* __restrict__ mu, const double* __restrict__ var,
+                                   int n_obj, long long n, HostParams p, HostParams q) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double a = 0.0;
+  for (int o = 0; o < n_obj; ++o) {
+    const long long off = (long long)o * n + i;
+    const double m = (mu[off] - p.a[o]) / q.a[o];      // (mu - pm) / sqrt(pv)
+    const double v = var[off] / p.b[o];                 // var / pv
+    const double u = m + p.c[o] * sqrt(fabs(v));        // mu + beta * sqrt(|var|)
+    if (smu) smu[off] = m;
+    if (svar) svar[off] = v;
+    if (ucb) ucb[off] = u;
+    a = (o == 0) ? u : a + u;
+  }
+  if (acq) acq[i] = a;
+}
+
+// ------------------------------------------------------------------------ selection
+struct SelArgs {
+  const double* acq;
+  long long n_cand, cand_offset;
+  int kind, dim, n_excl, topq;
+  const void* cand;
+  long long grid_lo[BO_MAX_DIM], grid_shape[BO_MAX_DIM];
+  const double* excl;
+  TopEntry* partial;
+};
+
+__device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int k) {
+  if (a.kind == BO_CAND_I64) return (double)((const long long*)a.cand)[j * a.dim + k];
+  if (a.kind == BO_CAND_F64) return ((const double*)a.cand)[j * a.dim + k];
+  long long gi = a.cand_offset + j;
+  for (int t = a.dim - 1; t > k; --t) gi /= a.grid_shape[t];
+  return (double)(a.grid_lo[k] + gi % a.grid_shape[k]);
+}
+
+// grid-stride over candidates; each wave folds 64 candidates per step into its running
+// top-q (4 inserts of 16), then writes its list to `partial`.
+__global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
+  __shared__ double ex[1024 * BO_MAX_DIM];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n_lds = a.n_excl <= 1024 ? a.n_excl : 0;
+  for (int t = threadIdx.x; t < n_lds * a.dim; t += blockDim.x) ex[t] = a.excl[t];
+  __syncthreads();
+  const double* exs = n_lds ? ex : a.excl;
+  double lv = -__builtin_inf();
+  long long li = -1;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long base = (long long)blockIdx.x * blockDim.x + wave * 64; base < a.n_cand;
+       base += stride) {
+    const long long j = base + lane;
+    double v = -__builtin_inf();
+    long long gi = -1;
+    if (j < a.n_cand) {
+      double c[BO_MAX_DIM];
+      for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
+      bool hit = false;
+      for (int e = 0; e < a.n_excl && !hit; ++e) {
+        bool eq = true;
+        for (int k = 0; k < a.dim; ++k) eq = eq && (exs[e * a.dim + k] == c[k]);
+        hit = eq;
+      }
+      v = a.acq[j];
+      gi = hit ? -1 : a.cand_offset + j;
+    }
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) {
+      const double nv = __shfl(v, (lane & 15) + 16 * grp, 64);
+      const long long ni = __shfl(gi, (lane & 15) + 16 * grp, 64);
+      bo_wave_topq_insert(lv, li, nv, ni, a.topq);
+    }
+  }
+  if (lane < a.topq) {
+    TopEntry* dst = a.partial + ((size_t)blockIdx.x * 4 + wave) * a.topq;
+    dst[lane].v = lv;
+    dst[lane].i = li;
+  }
+}
+
+__global__ __launch_bounds__(1024) void merge_kernel(const TopEntry* __restrict__ lists,
+                                                     int n_lists, int q, double* __restrict__ out_v,
+                                                     long long* __restrict__ out_i) {
+  __shared__ TopEntry stage[16 * BO_MAX_TOPQ];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  double lv = -__builtin_inf();
+  long long li = -1;
+  const long long total = (long long)n_lists * q;
+  for (long long base = (long long)wave * 16; base < total; base += (long long)nw * 16) {
+    double nv = -__builtin_inf();
+    long long ni = -1;
+    if (lane < 16 && base + lane < total) { nv = lists[base + lane].v; ni = lists[base + lane].i; }
+    bo_wave_topq_insert(lv, li, nv, ni, q);
+  }
+  if (lane < q) { stage[wave * q + lane].v = lv; stage[wave * q + lane].i = li; }
+  __syncthreads();
+  if (wave == 0) {
+    double fv = -__builtin_inf();
+    long long fi = -1;
+    for (int base = 0; base < nw * q; base += 16) {
+      double nv = -__builtin_inf();
+      long long ni = -1;
+      if (lane < 16 && base + lane < nw * q) { nv = stage[base + lane].v; ni = stage[base + lane].i; }
+      bo_wave_topq_insert(fv, fi, nv, ni, q);
+    }
+    if (lane < q) { out_v[lane] = fv; out_i[lane] = fi; }
+  }
+}
+
+// --------------------------------------------------------------------------- Pareto
+// mask[i] = 0 iff some row j (j != i) weakly dominates row i under maximisation:
+// y_j >= y_i in every objective and y_j > y_i in at least one (pareto.py:279-287 with
+// y negated).  Comparisons only: bit-exact, NaN never dominates nor is dominated.
+// The reference's scan order (break on the first dominator, marks only rows it
+// reaches) yields exactly this set; see oracle/oracle_np.py:is_pareto_efficient.
+__global__ __launch_bounds__(256) void pareto_kernel(const double* __restrict__ y, long long n,
+                                                     int n_obj, uint8_t* __restrict__ mask) {
+  __shared__ double tile[256 * BO_MAX_OBJ];
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  double yi[BO_MAX_OBJ];
+  for (int o = 0; o < BO_MAX_OBJ; ++o) yi[o] = (i < n && o < n_obj) ? y[i * n_obj + o] : 0.0;
+  bool dominated = false;
+  for (long long t0 = 0; t0 < n; t0 += 256) {
+    __syncthreads();
+    const long long tj = t0 + threadIdx.x;
+    for (int o = 0; o < n_obj; ++o) tile[threadIdx.x * n_obj + o] = tj < n ? y[tj * n_obj + o] : 0.0;
+    __syncthreads();
+    const int cnt = (int)(n - t0 < 256 ? n - t0 : 256);
+    if (i < n && !dominated) {
+      for (int t = 0; t < cnt; ++t) {
+        bool ge = true, gt = false;
+        for (int o = 0; o < n_obj; ++o) {
+          const double yj = tile[t * n_obj + o];
+          ge = ge && (yj >= yi[o]);
+          gt = gt || (yj > yi[o]);
+        }
+        if (ge && gt) { dominated = true; break; }
+      }
+    }
+  }
+  if (i < n) mask[i] = dominated ? 0 : 1;
+}
+
+int cus_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
+    cus = p.multiProcessorCount;
+  }
+  return cus;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bo_update_k(double* km, int64_t ld, int32_t n_obj, const double* x, int32_t dim,
+                int64_t last_eval, int64_t cur, const double* pv, const double* ls, void* stream) {
+  if (!km || !x || !pv || !ls || n_obj < 1 || n_obj > BO_MAX_OBJ || dim < 1 || ld < cur ||
+      last_eval < 0 || cur > (1 << 20))
+    return BO_ERR_ARG;
+  if (cur <= last_eval) return BO_OK;
+  HostParams p;
+  memset(&p, 0, sizeof(p));
+  for (int o = 0; o < n_obj; ++o) { p.a[o] = pv[o]; p.b[o] = ls[o] * ls[o]; }
+  const int rows = (int)(cur - last_eval);
+  dim3 grid((unsigned)((cur + 127) / 128), (unsigned)rows);
+  hipLaunchKernelGGL(gram_kernel, grid, dim3(128), 0, (hipStream_t)stream, km, (long long)ld,
+                     n_obj, x, dim, (int)last_eval, (int)cur, p);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+int bo_update_k_star(double* ks, int64_t ld_rows, int32_t n_obj, const double* x, int32_t dim,
+                     int32_t kind, const void* cand, int64_t n_cand, int64_t last_eval,
+                     int64_t cur, const double* pv, const double* ls, void* stream) {
+  if (!ks || !x || !cand || !pv || !ls || n_obj < 1 || n_obj > BO_MAX_OBJ || dim < 1 ||
+      ld_rows < cur || (kind != BO_CAND_I64 && kind != BO_CAND_F64) || last_eval < 0)
+    return BO_ERR_ARG;
+  if (cur <= last_eval || n_cand == 0) return BO_OK;
+  HostParams p;
+  memset(&p, 0, sizeof(p));
+  for (int o = 0; o < n_obj; ++o) { p.a[o] = pv[o]; p.b[o] = ls[o] * ls[o]; }
+  dim3 grid((unsigned)((n_cand + 255) / 256), (unsigned)(cur - last_eval));
+  hipLaunchKernelGGL(kstar_kernel, grid, dim3(256), 0, (hipStream_t)stream, ks,
+                     (long long)ld_rows, n_obj, x, dim, kind, cand, (long long)n_cand,
+                     (int)last_eval, (int)cur, p);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+int bo_standardize_ucb_hvi(double* smu, double* svar, double* ucb, double* acq, const double* mu,
+                           const double* var, int32_t n_obj, int64_t n, const double* pm,
+                           const double* pv, const double* betas, void* stream) {
+  if (!mu || !var || !pm || !pv || !betas || n_obj < 1 || n_obj > BO_MAX_OBJ || n < 0)
+    return BO_ERR_ARG;
+  if (n == 0) return BO_OK;
+  HostParams p, q;
+  memset(&p, 0, sizeof(p));
+  memset(&q, 0, sizeof(q));
+  for (int o = 0; o < n_obj; ++o) {
+    p.a[o] = pm[o];
+    p.b[o] = pv[o];
+    p.c[o] = betas[o];
+    q.a[o] = sqrt(pv[o]);
+  }
+  hipLaunchKernelGGL(std_ucb_hvi_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, smu, svar, ucb, acq, mu, var, n_obj, (long long)n, p, q);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+size_t bo_select_topq_workspace_size(int64_t n_cand, int32_t topq) {
+  (void)n_cand;
+  return (size_t)1024 * 4 * (topq > 0 ? topq : 1) * sizeof(TopEntry);
+}
+
+int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* cand,
+                   const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
+                   int64_t cand_offset, const double* excl, int64_t n_excl, int32_t topq,
+                   double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes, void* stream) {
+  if (!acq || topq < 1 || topq > BO_MAX_TOPQ || dim < 1 || dim > BO_MAX_DIM || n_cand < 0 ||
+      !top_val || !top_idx || (n_excl > 0 && !excl) || kind < 0 || kind > 2)
+    return BO_ERR_ARG;
+  if (kind != BO_CAND_GRID && !cand) return BO_ERR_ARG;
+  if (kind == BO_CAND_GRID && (!grid_lo || !grid_shape)) return BO_ERR_ARG;
+  if (!ws || ws_bytes < bo_select_topq_workspace_size(n_cand, topq)) return BO_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  SelArgs a;
+  memset(&a, 0, sizeof(a));
+  a.acq = acq;
+  a.n_cand = n_cand;
+  a.cand_offset = cand_offset;
+  a.kind = kind;
+  a.dim = dim;
+  a.n_excl = (int)n_excl;
+  a.topq = topq;
+  a.cand = cand;
+  for (int k = 0; k < BO_MAX_DIM; ++k) a.grid_shape[k] = 1;
+  if (kind == BO_CAND_GRID)
+    for (int k = 0; k < dim; ++k) {
+      if (grid_shape[k] <= 0) return BO_ERR_ARG;
+      a.grid_lo[k] = grid_lo[k];
+      a.grid_shape[k] = grid_shape[k];
+    }
+  a.excl = excl;
+  a.partial = (TopEntry*)ws;
+  long long blocks = (n_cand + 255) / 256;
+  const int max_blocks = cus_count() * 4 < 1024 ? cus_count() * 4 : 1024;
+  if (blocks > max_blocks) blocks = max_blocks;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(select_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  BO_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
+                     (int)blocks * 4, topq, top_val, (long long*)top_idx);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+int bo_pareto_mask(const double* y, int64_t n, int32_t n_obj, uint8_t* mask, void* stream) {
+  if (!y || !mask || n < 0 || n_obj < 1 || n_obj > BO_MAX_OBJ) return BO_ERR_ARG;
+  if (n == 0) return BO_OK;
+  hipLaunchKernelGGL(pareto_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, y, (long long)n, n_obj, mask);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+}  // extern "C"

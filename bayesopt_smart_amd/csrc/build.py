@@ -1,0 +1,70 @@
+"""Build libbo_amd.so in-tree with hipcc for gfx950 (no torch involvement).
+
+    python -m bayesopt_smart_amd.csrc.build        # or via __graft_entry__.build()
+
+Objects are cached by source mtime under csrc/build/; `-j` parallel compiles.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+LIB = os.path.join(PKG, "libbo_amd.so")
+BUILD = os.path.join(HERE, "build")
+SOURCES = ["bo_predict.hip", "bo_fit.hip", "bo_select.hip", "bo_misc.hip"]
+HEADERS = ["bo_common.h", os.path.join("..", "..", "include", "bo_amd.h")]
+ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         "-I", os.path.join(ROOT, "include")]
+
+
+def _hipcc():
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def _newest_header():
+    return max(os.path.getmtime(os.path.join(HERE, h)) for h in HEADERS)
+
+
+def _compile(src, hdr_mtime):
+    s = os.path.join(HERE, src)
+    o = os.path.join(BUILD, src + ".o")
+    if os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), hdr_mtime):
+        return o, False
+    cmd = [_hipcc(), *FLAGS, "-c", s, "-o", o]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return o, True
+
+
+def build(verbose=True, jobs=None):
+    os.makedirs(BUILD, exist_ok=True)
+    hdr = _newest_header()
+    jobs = jobs or min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        results = list(ex.map(lambda s: _compile(s, hdr), SOURCES))
+    objs = [o for o, _ in results]
+    rebuilt = any(r for _, r in results)
+    if rebuilt or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+        if verbose:
+            print(f"built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

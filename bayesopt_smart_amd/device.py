@@ -1,0 +1,58 @@
+"""Device plumbing: HIP device checks, stream handles, cached workspaces.
+
+PyTorch-ROCm is used only for device memory, streams and torch.distributed; every
+computation on the hot path is a libbo_amd.so kernel.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+F64 = torch.float64
+
+
+def require_device(device=None):
+    """Return a torch.device on a HIP GPU or raise (no CPU fallback on the product path)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("bayesopt_smart_amd needs a HIP device (torch.cuda.is_available() is False)")
+    _lib.load()
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise RuntimeError(f"bayesopt_smart_amd tensors must live on a HIP device, got {dev}")
+    return dev
+
+
+def stream_handle(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def as_dev(x, device, dtype=F64):
+    """Tensor on `device` with `dtype`, C-contiguous (copies only when needed)."""
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=device, dtype=dtype)
+    else:
+        t = torch.as_tensor(x, dtype=dtype, device=device)
+    return t.contiguous()
+
+
+class Workspace:
+    """Grow-only device scratch buffer (one per device)."""
+
+    _cache = {}
+
+    @classmethod
+    def get(cls, nbytes, device):
+        key = (device.type, device.index)
+        buf = cls._cache.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            cls._cache[key] = buf
+        return buf

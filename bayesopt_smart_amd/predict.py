@@ -1,0 +1,203 @@
+"""Fused GP predict + acquisition over a candidate set (the north-star hot path).
+
+``predict_acquire`` is the host side of ``bo_predict_acquire`` (include/bo_amd.h): one
+call scores a shard of candidates -- posterior mean and variance
+(bayesopt/numba_kernels.py:450-535), standardisation (:538-570), per-objective UCB and
+the reference's summed-UCB "hypervolume improvement" (bayesopt/acquisition.py:33-108) --
+and returns the shard's top-q selection with evaluated points excluded
+(bayesopt/acquisition.py:116-144).  No N x M k_star array exists anywhere.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .device import F64, Workspace, as_dev, ptr, require_device, stream_handle
+
+OUTPUT_NAMES = ("mu", "var", "std_mu", "std_var", "ucb", "acq")
+
+
+@dataclass
+class CandidateSet:
+    """Candidates scored by the hot path.
+
+    kind ``grid``: the reference's integer 'ij' meshgrid (bayesian_optimization.py:338-340),
+    generated on the device from the linear index (no candidate array in HBM);
+    kind ``i64``/``f64``: an explicit [M, d] device array (the reference's input_space, or
+    e.g. a Sobol set).
+    """
+
+    kind: str
+    n: int
+    dim: int
+    tensor: Optional[torch.Tensor] = None
+    lo: Optional[Sequence[int]] = None
+    shape: Optional[Sequence[int]] = None
+
+    @staticmethod
+    def grid(bounds):
+        lo = [int(b[0]) for b in bounds]
+        shape = [int(b[1]) - int(b[0]) for b in bounds]
+        n = int(np.prod(shape, dtype=np.int64))
+        return CandidateSet("grid", n, len(bounds), lo=lo, shape=shape)
+
+    @staticmethod
+    def explicit(points, device=None):
+        dev = require_device(device)
+        if isinstance(points, torch.Tensor):
+            is_int = not points.is_floating_point()
+        else:
+            points = np.asarray(points)
+            is_int = np.issubdtype(points.dtype, np.integer)
+        dtype = torch.int64 if is_int else F64
+        t = as_dev(points, dev, dtype)
+        if t.dim() != 2:
+            raise ValueError("candidates must be [M, d]")
+        return CandidateSet("i64" if is_int else "f64", t.shape[0], t.shape[1], tensor=t)
+
+    @property
+    def kind_code(self):
+        return {"i64": _lib.CAND_I64, "f64": _lib.CAND_F64, "grid": _lib.CAND_GRID}[self.kind]
+
+    def points(self, idx):
+        """Coordinates of global candidate indices (numpy [k, d]; int64 for grid/i64)."""
+        idx = np.asarray(idx, dtype=np.int64)
+        if self.kind == "grid":
+            out = np.empty((idx.size, self.dim), dtype=np.int64)
+            rem = idx.copy()
+            for k in range(self.dim - 1, -1, -1):
+                out[:, k] = self.lo[k] + rem % self.shape[k]
+                rem //= self.shape[k]
+            return out
+        return self.tensor[torch.as_tensor(idx, device=self.tensor.device)].cpu().numpy()
+
+    def materialize(self, device=None):
+        """Explicit int64 [M, d] tensor of a grid (the reference's input_space)."""
+        if self.kind != "grid":
+            return self.tensor
+        dev = require_device(device)
+        ranges = [torch.arange(l, l + s, device=dev, dtype=torch.int64) for l, s in zip(self.lo, self.shape)]
+        mesh = torch.meshgrid(*ranges, indexing="ij")
+        return torch.stack([m.reshape(-1) for m in mesh], dim=-1).contiguous()
+
+
+def _fill_desc(x_train, y_train, kinv, cands, pm, pv, ls, betas, offset, count, excl, topq):
+    d = _lib.PredictDesc()
+    n_obj = len(pm)
+    if not 1 <= n_obj <= _lib.MAX_OBJ:
+        raise ValueError(f"n_objectives must be in [1, {_lib.MAX_OBJ}]")
+    if not 1 <= cands.dim <= _lib.MAX_DIM:
+        raise ValueError(f"dimension must be in [1, {_lib.MAX_DIM}]")
+    n = x_train.shape[0]
+    d.n_obj = n_obj
+    d.dim = cands.dim
+    d.n_train = n
+    d.x_train = ptr(x_train)
+    d.y_train = ptr(y_train)
+    d.ld_y = y_train.stride(0)
+    d.kinv = ptr(kinv)
+    d.ld_k = kinv.shape[-1]
+    d.cand_kind = cands.kind_code
+    d.n_cand = count
+    d.cand_offset = offset
+    if cands.kind == "grid":
+        for k in range(cands.dim):
+            d.grid_lo[k] = cands.lo[k]
+            d.grid_shape[k] = cands.shape[k]
+        d.cand = None
+    else:
+        # explicit candidates: the call sees rows [offset, offset + count)
+        d.cand = cands.tensor.data_ptr() + offset * cands.dim * cands.tensor.element_size()
+        d.cand_offset = offset
+    if excl is not None:
+        d.excl_points = ptr(excl)
+        d.n_excl = excl.shape[0]
+    for o in range(n_obj):
+        d.prior_mean[o] = float(pm[o])
+        d.prior_var[o] = float(pv[o])
+        d.length_scale[o] = float(ls[o])
+        d.beta[o] = float(betas[o])
+    d.topq = topq
+    return d
+
+
+def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, prior_variance,
+                    length_scales, betas, *, outputs=("mu", "var", "acq"), topq=0,
+                    excl_points=None, offset=0, count=None, out=None, device=None):
+    """Score candidates [offset, offset+count) of `cands`.
+
+    x_train [N, d], y_train [N or T, n_obj] (only the first N rows are read), kinv
+    [n_obj, N, N] (invert_k output) -- device f64 tensors or arrays.  Returns a dict with
+    the requested outputs (device tensors [n_obj, count] / [count]) and, if topq > 0,
+    ``top_val`` / ``top_idx`` (device [topq]; index -1 = no candidate).  Asynchronous
+    on the current stream.
+    """
+    dev = require_device(device)
+    x_train = as_dev(x_train, dev)
+    y_train = as_dev(y_train, dev)
+    kinv = as_dev(kinv, dev)
+    n, n_obj = x_train.shape[0], len(prior_mean)
+    if kinv.dim() != 3 or kinv.shape[0] != n_obj or kinv.shape[1] != kinv.shape[2] or kinv.shape[1] < n:
+        raise ValueError("kinv must be [n_obj, >=N, >=N]")
+    if y_train.shape[0] < n or y_train.shape[1] < n_obj:
+        raise ValueError("y_train must be [>=N, n_obj]")
+    if x_train.shape[1] != cands.dim:
+        raise ValueError("x_train / candidate dimension mismatch")
+    count = cands.n - offset if count is None else count
+    if excl_points is not None:
+        excl_points = as_dev(excl_points, dev)
+    if not 0 <= topq <= _lib.MAX_TOPQ:
+        raise ValueError(f"topq must be in [0, {_lib.MAX_TOPQ}]")
+    desc = _fill_desc(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
+                      betas, offset, count, excl_points, topq)
+    res = {} if out is None else dict(out)
+    for name in outputs:
+        if name not in OUTPUT_NAMES:
+            raise ValueError(f"unknown output {name}")
+        if name not in res:
+            shape = (count,) if name == "acq" else (n_obj, count)
+            res[name] = torch.empty(shape, dtype=F64, device=dev)
+    ld_out = None
+    for name in ("mu", "var", "std_mu", "std_var", "ucb"):
+        t = res.get(name)
+        if t is not None:
+            if t.dim() != 2 or t.shape[0] != n_obj or t.stride(1) != 1 or t.shape[1] < count:
+                raise ValueError(f"{name} must be [n_obj, >=count] with unit column stride")
+            if ld_out is not None and t.stride(0) != ld_out:
+                raise ValueError("all per-objective outputs must share one row stride")
+            ld_out = t.stride(0)
+            setattr(desc, name, t.data_ptr())
+    if res.get("acq") is not None:
+        desc.acq = res["acq"].data_ptr()
+    desc.ld_out = ld_out or count
+    if topq:
+        res["top_val"] = torch.empty(topq, dtype=F64, device=dev)
+        res["top_idx"] = torch.empty(topq, dtype=torch.int64, device=dev)
+        desc.top_val = res["top_val"].data_ptr()
+        desc.top_idx = res["top_idx"].data_ptr()
+    lib = _lib.load()
+    nbytes = lib.bo_predict_workspace_size(desc)
+    if nbytes == 0:
+        raise _lib.BoNativeError(_lib.ERR_ARG, "bo_predict_workspace_size")
+    ws = Workspace.get(nbytes, dev)
+    _lib.check(lib.bo_predict_acquire(desc, ws.data_ptr(), ws.numel(), stream_handle(dev)),
+               "bo_predict_acquire")
+    res["_keepalive"] = (x_train, y_train, kinv, excl_points)
+    return res
+
+
+def merge_topq(vals, idxs, q):
+    """Host merge of per-shard top-q lists in the selection order of select_next_batch:
+    NaN first, then descending value, ties by ascending global index; index -1 dropped."""
+    vals = np.asarray(vals, dtype=np.float64).ravel()
+    idxs = np.asarray(idxs, dtype=np.int64).ravel()
+    keep = idxs >= 0
+    vals, idxs = vals[keep], idxs[keep]
+    nan = np.isnan(vals)
+    order = np.lexsort((idxs, -np.where(nan, 0.0, vals), ~nan))
+    return vals[order][:q], idxs[order][:q]

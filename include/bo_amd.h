@@ -1,0 +1,197 @@
+/*
+ * bo_amd.h — C ABI of the MI355X-native GP-predict + acquisition hot path.
+ *
+ * Drop-in boundary for alebal123bal/BayesOpt_smart's inner loop
+ * (bayesopt/bayesian_optimization.py:129-207, the functions it imports by name at
+ * :24-42).  Every entry point names the reference function it replaces.
+ *
+ * Conventions (all entry points):
+ *   - plain pointers and sizes; no torch / HIP types in the signatures;
+ *   - "device" pointers are HIP device memory owned by the caller (the library never
+ *     allocates or frees caller memory); "host" pointers are read during the call;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream); every call is
+ *     asynchronous on that stream unless stated otherwise;
+ *   - the return value is a bo_status; no C++ exception crosses the ABI.
+ *   - all floating point is IEEE binary64 (the reference's NUMBA_FLOAT_TYPE,
+ *     bayesopt/config.py:54).
+ */
+#ifndef BO_AMD_H
+#define BO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BO_ABI_VERSION 1
+#define BO_MAX_OBJ 8      /* objectives per call                              */
+#define BO_MAX_DIM 8      /* input dimensions                                 */
+#define BO_MAX_TOPQ 48    /* batch size of the fused top-q selection          */
+
+typedef enum bo_status {
+  BO_OK = 0,
+  BO_ERR_ARG = 1,          /* invalid argument / shape                          */
+  BO_ERR_UNSUPPORTED = 2,  /* valid but outside what this build implements       */
+  BO_ERR_WORKSPACE = 3,    /* workspace missing or too small                     */
+  BO_ERR_HIP = 4,          /* a HIP runtime call failed                          */
+  BO_ERR_NOT_PD = 5,       /* matrix not positive definite (np.linalg.LinAlgError) */
+  BO_ERR_SINGULAR = 6      /* singular matrix (np.linalg.LinAlgError)            */
+} bo_status;
+
+typedef enum bo_cand_kind {
+  BO_CAND_I64 = 0,   /* explicit candidates, int64 [n_cand][dim] (the reference's input_space) */
+  BO_CAND_F64 = 1,   /* explicit candidates, f64 [n_cand][dim] (e.g. a Sobol set)            */
+  BO_CAND_GRID = 2   /* implicit 'ij' integer grid: bayesian_optimization.py:338-340           */
+} bo_cand_kind;
+
+int bo_abi_version(void);
+const char* bo_status_string(int status);
+/* number of HIP devices visible; <0 on HIP error (no compute launched) */
+int bo_device_count(void);
+
+/* ------------------------------------------------------------------------------------
+ * Fused GP predict + acquisition + top-q:   replaces, for one candidate shard,
+ *   update_k_star     bayesopt/numba_kernels.py:406-442
+ *   update_mean       bayesopt/numba_kernels.py:450-488
+ *   update_variance   bayesopt/numba_kernels.py:491-535
+ *   standardize_objectives                 :538-570
+ *   update_ucb        bayesopt/acquisition.py:55-81
+ *   update_hypervolume_improvement         bayesopt/acquisition.py:89-108
+ *   select_next_batch bayesopt/acquisition.py:116-144 (local top-q with exclusion)
+ * No N x M k_star array is materialised: candidate tiles are generated, contracted
+ * against K^-1 on the f64 matrix cores and reduced to outputs in one pass.
+ * ---------------------------------------------------------------------------------- */
+typedef struct bo_predict_desc {
+  int32_t n_obj;              /* objectives (<= BO_MAX_OBJ)                                 */
+  int32_t dim;                /* input dimensions (<= BO_MAX_DIM)                            */
+  int64_t n_train;            /* N = current_eval                                            */
+  const double* x_train;      /* device [n_train][dim] (x_vector[:N])                        */
+  const double* y_train;      /* device, y_vector rows with row stride ld_y (>= n_obj)        */
+  int64_t ld_y;
+  const double* kinv;         /* device [n_obj][ld_k][ld_k]; leading N x N block = invert_k() */
+  int64_t ld_k;
+  int32_t cand_kind;          /* bo_cand_kind                                                 */
+  int32_t reserved0;
+  const void* cand;           /* device [n_cand][dim] (kinds I64/F64)                         */
+  int64_t n_cand;             /* candidates scored by this call                               */
+  int64_t cand_offset;        /* global index of this call's first candidate                  */
+  int64_t grid_lo[BO_MAX_DIM];     /* kind GRID: lower bound of each axis                    */
+  int64_t grid_shape[BO_MAX_DIM];  /* kind GRID: points per axis (axis dim-1 fastest)        */
+  const double* excl_points;  /* device [n_excl][dim] evaluated points; NULL = x_train        */
+  int64_t n_excl;
+  double prior_mean[BO_MAX_OBJ];
+  double prior_var[BO_MAX_OBJ];
+  double length_scale[BO_MAX_OBJ];
+  double beta[BO_MAX_OBJ];
+  /* optional device outputs (NULL = not written); per-objective arrays are
+   * [n_obj][ld_out] and this call writes columns [0, n_cand) of each row. */
+  double* mu;                 /* mu_objectives             */
+  double* var;                /* variance_objectives       */
+  double* std_mu;             /* std_mu_objectives         */
+  double* std_var;            /* std_variance_objectives   */
+  double* ucb;                /* ucb                       */
+  double* acq;                /* acquisition_values [n_cand] */
+  int64_t ld_out;
+  /* top-q selection of this call's candidates (0 = none), ordered NaN first, then
+   * descending acquisition value, ties by ascending global index; candidates equal to
+   * an evaluated point are skipped.  Device outputs. */
+  int32_t topq;
+  int32_t reserved1;
+  double* top_val;            /* [topq]                                          */
+  int64_t* top_idx;           /* [topq] global candidate index, -1 = no candidate */
+} bo_predict_desc;
+
+/* bytes of device workspace bo_predict_acquire needs for `desc` (0 on bad args) */
+size_t bo_predict_workspace_size(const bo_predict_desc* desc);
+int bo_predict_acquire(const bo_predict_desc* desc, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Unfused drop-ins with the reference's in-place semantics (device arrays).
+ * ---------------------------------------------------------------------------------- */
+
+/* update_k  bayesopt/numba_kernels.py:329-367: kernel_matrix[o][i][j] for
+ * last_eval <= i < current_eval, i <= j < current_eval, then mirror.
+ * kernel_matrix: device [n_obj][ld][ld]; x: device [*][dim]. prior_variance/length_scales host. */
+int bo_update_k(double* kernel_matrix, int64_t ld, int32_t n_obj, const double* x, int32_t dim,
+                int64_t last_eval, int64_t current_eval, const double* prior_variance,
+                const double* length_scales, void* stream);
+
+/* update_k_star  bayesopt/numba_kernels.py:406-442: k_star device [n_obj][ld_rows][n_cand];
+ * candidates: explicit int64/f64 device array (kind I64/F64). Rows [last_eval, current_eval). */
+int bo_update_k_star(double* k_star, int64_t ld_rows, int32_t n_obj, const double* x, int32_t dim,
+                     int32_t cand_kind, const void* cand, int64_t n_cand, int64_t last_eval,
+                     int64_t current_eval, const double* prior_variance,
+                     const double* length_scales, void* stream);
+
+/* update_mean + update_variance (numba_kernels.py:450-535) from a materialised k_star
+ * (device [n_obj][ld_rows][n_cand]).  mu/var: device [n_obj][n_cand] (either may be NULL). */
+int bo_update_mean_variance(double* mu, double* var, const double* k_star, int64_t ld_rows,
+                            int32_t n_obj, int64_t n_cand, const double* kinv, int64_t ld_k,
+                            const double* y, int64_t ld_y, int64_t current_eval,
+                            const double* prior_mean, const double* prior_variance,
+                            void* workspace, size_t workspace_bytes, void* stream);
+size_t bo_update_mean_variance_workspace_size(int32_t n_obj, int64_t current_eval);
+
+/* standardize_objectives + update_ucb + update_hypervolume_improvement
+ * (numba_kernels.py:538-570, acquisition.py:55-108): elementwise over [n_obj][n_cand].
+ * Any output may be NULL. */
+int bo_standardize_ucb_hvi(double* std_mu, double* std_var, double* ucb, double* acq,
+                           const double* mu, const double* var, int32_t n_obj, int64_t n_cand,
+                           const double* prior_mean, const double* prior_variance,
+                           const double* betas, void* stream);
+
+/* select_next_batch  bayesopt/acquisition.py:116-144 over an acquisition array:
+ * top-q (q <= BO_MAX_TOPQ) skipping candidates equal to any evaluated point. */
+int bo_select_topq(const double* acq, int64_t n_cand, int32_t cand_kind, const void* cand,
+                   const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
+                   int64_t cand_offset, const double* excl_points, int64_t n_excl, int32_t topq,
+                   double* top_val, int64_t* top_idx, void* workspace, size_t workspace_bytes,
+                   void* stream);
+size_t bo_select_topq_workspace_size(int64_t n_cand, int32_t topq);
+
+/* is_pareto_efficient  bayesopt/pareto.py:12-45: mask[i] = 1 iff no row j dominates row i
+ * (maximisation, weak dominance; NaN rows never dominate nor are dominated).
+ * y: device [n][n_obj] row-major; mask: device uint8 [n]. Bit-exact. */
+int bo_pareto_mask(const double* y, int64_t n, int32_t n_obj, uint8_t* mask, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * GP fit on device.
+ * ---------------------------------------------------------------------------------- */
+
+/* invert_k  bayesopt/numba_kernels.py:370-403: out[o] = inv(K[o][:N,:N] + 1e-6 I) by LU with
+ * partial pivoting (LAPACK gesv semantics).  kernel_matrix device [n_obj][ld][ld];
+ * out device [n_obj][n][n]. Returns BO_ERR_SINGULAR on an exactly singular pivot.
+ * Synchronous (the status depends on the factorisation). */
+int bo_invert_k(double* out, const double* kernel_matrix, int64_t ld, int32_t n_obj, int64_t n,
+                void* workspace, size_t workspace_bytes, void* stream);
+size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n);
+
+/* compute_mll  bayesopt/numba_kernels.py:152-235 (Gram rebuilt into kernel_matrix first, as
+ * the reference does).  Writes the summed MLL to *mll_out (host).  Returns BO_ERR_NOT_PD when
+ * a Cholesky pivot is not positive.  Synchronous. */
+int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* y, int64_t ld_y,
+                   double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
+                   const double* prior_variance, const double* length_scales,
+                   int64_t current_eval, void* workspace, size_t workspace_bytes, void* stream);
+size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n);
+
+/* ------------------------------------------------------------------------------------
+ * Measurement hooks (bench.py): while enabled, each fused predict kernel launch (the
+ * dominant kernel of bo_predict_acquire) is bracketed by HIP events on its stream;
+ * bo_profile_stop synchronises them and returns the summed kernel time.
+ * ---------------------------------------------------------------------------------- */
+int bo_profile_start(int max_launches);
+int bo_profile_stop(double* total_ms, int* launches);
+
+/* ------------------------------------------------------------------------------------
+ * Self test: D[16][16] = A[16][4] * B[4][16] on one f64 MFMA (layout check). Device ptrs.
+ * ---------------------------------------------------------------------------------- */
+int bo_selftest_mfma_f64(const double* a16x4, const double* b4x16, double* d16x16, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BO_AMD_H */

@@ -1,0 +1,169 @@
+"""GPU parity of the fused predict + acquisition kernel (bo_predict_acquire) against the
+reference's own outputs (tests/golden/*.npz) and the CPU oracle (oracle/oracle_np.py)."""
+
+import numpy as np
+import pytest
+
+from oracle import oracle_np as O
+from parity import check_predict, check_topq
+from conftest import predict_fixture
+
+pytestmark = pytest.mark.gpu
+
+ALL = ("mu", "var", "std_mu", "std_var", "ucb", "acq")
+
+
+@pytest.fixture(scope="module")
+def bo():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import bayesopt_smart_amd as bo
+    bo._lib.load()
+    return bo
+
+
+def _run(bo, d, cands, q=16, outputs=ALL, excl=None):
+    import torch
+    res = bo.predict.predict_acquire(d["x"], d["y"], d["Kinv"], cands, d["pm"], d["pv"], d["ls"],
+                                     d["betas"], outputs=outputs, topq=q, excl_points=excl)
+    torch.cuda.synchronize()
+    out = {k: v.cpu().numpy() for k, v in res.items() if not k.startswith("_")}
+    return out
+
+
+def _excluded(cand_pts, x):
+    xs = {tuple(r) for r in np.asarray(x, dtype=np.float64)}
+    return np.array([tuple(np.asarray(c, dtype=np.float64)) in xs for c in cand_pts])
+
+
+def test_mfma_f64_layout(bo):
+    import torch
+    rng = np.random.default_rng(1)
+    a = rng.integers(-8, 8, size=(16, 4)).astype(np.float64)
+    b = rng.integers(-8, 8, size=(4, 16)).astype(np.float64)   # asymmetric
+    ta, tb = torch.tensor(a, device="cuda"), torch.tensor(b, device="cuda")
+    td = torch.empty((16, 16), dtype=torch.float64, device="cuda")
+    bo._lib.check(bo._lib.load().bo_selftest_mfma_f64(ta.data_ptr(), tb.data_ptr(), td.data_ptr(), None), "selftest")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(td.cpu().numpy(), a @ b)
+
+
+@pytest.mark.parametrize("name", ["g1_predict_2d", "g2_predict_512", "g3_predict_6d3o"])
+def test_predict_vs_reference_golden(bo, name):
+    d = predict_fixture(name)
+    cands = bo.predict.CandidateSet.explicit(d["cand"])
+    out = _run(bo, d, cands)
+    check_predict(out, d, d["pv"])
+    excl = _excluded(d["cand"], d["x"])
+    check_topq(out["top_idx"], d["acq"], excl, 16)
+    # the reference's own batch (acquisition.py:116-144) for q = 3 and q = 16
+    for q in (3, 16):
+        ref_sel = d[f"select_q{q}"]
+        got = cands.points(out["top_idx"][:q])
+        gaps = np.sort(d["acq"][~excl])[::-1]
+        if np.all(np.abs(np.diff(gaps[: q + 1])) > 1e-4 * np.maximum(1.0, np.abs(gaps[:q]))):
+            np.testing.assert_array_equal(got.astype(np.float64), ref_sel.astype(np.float64))
+
+
+def test_predict_implicit_grid(bo):
+    d = predict_fixture("g1_grid")
+    cands = bo.predict.CandidateSet.grid([(0, int(d["grid_shape"][0])), (0, int(d["grid_shape"][1]))])
+    out = _run(bo, d, cands)
+    check_predict(out, d, d["pv"])
+    check_topq(out["top_idx"], d["acq"], _excluded(d["cand"], d["x"]), 16)
+    np.testing.assert_array_equal(cands.points(out["top_idx"][:3]), d["select_q3"])
+
+
+@pytest.mark.parametrize("n,dim,n_obj", [(7, 2, 2), (33, 3, 1), (130, 5, 4), (600, 2, 2), (1100, 6, 3)])
+def test_predict_shapes_vs_oracle(bo, n, dim, n_obj):
+    rng = np.random.default_rng(n)
+    m = 3000
+    cand = rng.integers(0, 60, size=(m, dim)).astype(np.int64)
+    x = rng.integers(0, 60, size=(n, dim)).astype(np.float64)
+    x[: n // 3] = cand[rng.choice(m, n // 3, replace=False)]          # some evaluated candidates
+    y = rng.normal(size=(n, n_obj)) * 50 + 10
+    pm, pv = y.mean(0), y.var(0)
+    ls = rng.uniform(3.0, 9.0, size=n_obj)
+    betas = rng.uniform(0.5, 2.5, size=n_obj)
+    km = np.zeros((n_obj, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    kinv = O.invert_k(n, km)
+    ref = O.predict_acquire(x, y, cand, pm, pv, ls, betas, kinv=kinv)
+    d = dict(x=x, y=y, Kinv=kinv, pm=pm, pv=pv, ls=ls, betas=betas)
+    out = _run(bo, d, bo.predict.CandidateSet.explicit(cand), q=8)
+    check_predict(out, ref, pv)
+    check_topq(out["top_idx"], ref["acq"], _excluded(cand, x), 8)
+
+
+def test_sharded_calls_match_single_call(bo):
+    """Candidate shards (the multi-GPU partition) reproduce the single-call result."""
+    d = predict_fixture("g1_predict_2d")
+    cands = bo.predict.CandidateSet.explicit(d["cand"])
+    full = _run(bo, d, cands, q=16)
+    vals, idxs, accs = [], [], []
+    import torch
+    m = cands.n
+    for lo in range(0, m, 1000):
+        cnt = min(1000, m - lo)
+        r = bo.predict.predict_acquire(d["x"], d["y"], d["Kinv"], cands, d["pm"], d["pv"], d["ls"], d["betas"],
+                                       outputs=("acq",), topq=16, offset=lo, count=cnt)
+        torch.cuda.synchronize()
+        vals.append(r["top_val"].cpu().numpy())
+        idxs.append(r["top_idx"].cpu().numpy())
+        accs.append(r["acq"].cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate(accs), full["acq"])
+    v, i = bo.predict.merge_topq(np.concatenate(vals), np.concatenate(idxs), 16)
+    np.testing.assert_array_equal(i, full["top_idx"])
+
+
+def test_edge_cases(bo):
+    import torch
+    d = predict_fixture("g1_predict_2d")
+    # empty candidate set
+    cands = bo.predict.CandidateSet.explicit(d["cand"][:0].reshape(0, 2))
+    r = bo.predict.predict_acquire(d["x"], d["y"], d["Kinv"], cands, d["pm"], d["pv"], d["ls"], d["betas"], topq=3)
+    torch.cuda.synchronize()
+    assert (r["top_idx"].cpu().numpy() == -1).all()
+    # every candidate evaluated -> nothing selectable
+    sub = d["cand"][:50]
+    cands = bo.predict.CandidateSet.explicit(sub)
+    r = bo.predict.predict_acquire(d["x"], d["y"], d["Kinv"], cands, d["pm"], d["pv"], d["ls"], d["betas"],
+                                   topq=3, excl_points=sub.astype(np.float64))
+    torch.cuda.synchronize()
+    assert (r["top_idx"].cpu().numpy() == -1).all()
+    # fewer selectable than q: only the non-excluded ones, in order
+    r = bo.predict.predict_acquire(d["x"], d["y"], d["Kinv"], cands, d["pm"], d["pv"], d["ls"], d["betas"],
+                                   topq=5, excl_points=sub[2:].astype(np.float64))
+    torch.cuda.synchronize()
+    got = r["top_idx"].cpu().numpy()
+    assert sorted(got[:2].tolist()) == [0, 1] and (got[2:] == -1).all()
+
+
+def test_full_size_c3_properties(bo):
+    """C3 at full size (N=512, M=1024^2 implicit grid): subsample parity against the oracle,
+    top-q consistent with the acq array, deterministic across runs."""
+    import torch
+    rng = np.random.default_rng(0)
+    side = 1024
+    lin = rng.choice(side * side, size=512, replace=False)
+    x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+    y = np.stack([-(x[:, 0] - 150) ** 2 + 100, -(x[:, 1] - 150) ** 2 + 20], axis=1)
+    pm, pv = y.mean(0), y.var(0)
+    ls, betas = np.array([20.0, 20.0]), np.array([2.0, 2.0])
+    km = np.zeros((2, 512, 512))
+    O.update_k(km, x, 0, 512, pv, ls)
+    kinv = O.invert_k(512, km)
+    d = dict(x=x, y=y, Kinv=kinv, pm=pm, pv=pv, ls=ls, betas=betas)
+    cands = bo.predict.CandidateSet.grid([(0, side), (0, side)])
+    out = _run(bo, d, cands, q=16, outputs=("mu", "var", "acq"))
+    out2 = _run(bo, d, cands, q=16, outputs=("acq",))
+    np.testing.assert_array_equal(out["acq"], out2["acq"])
+    np.testing.assert_array_equal(out["top_idx"], out2["top_idx"])
+    sub = np.sort(rng.choice(side * side, size=4096, replace=False))
+    pts = cands.points(sub)
+    ref = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv)
+    check_predict({k: (out[k][..., sub]) for k in ("mu", "var", "acq")}, ref, pv)
+    excl = np.zeros(side * side, dtype=bool)
+    excl[lin] = True
+    check_topq(out["top_idx"], out["acq"], excl, 16)
