@@ -69,6 +69,8 @@ _SIGS = {
     "bo_update_mean_variance_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
     "bo_standardize_ucb_hvi": (C.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, C.c_int32, C.c_int64,
                                          c_dbl_p, c_dbl_p, c_dbl_p, c_vp]),
+    "bo_update_ucb": (C.c_int, [c_vp, c_vp, c_vp, C.c_int32, C.c_int64, c_dbl_p, c_vp]),
+    "bo_update_hypervolume_improvement": (C.c_int, [c_vp, c_vp, C.c_int32, C.c_int64, c_vp]),
     "bo_select_topq": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, C.POINTER(C.c_int64),
                                  C.POINTER(C.c_int64), C.c_int32, C.c_int64, c_vp, C.c_int64,
                                  C.c_int32, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),

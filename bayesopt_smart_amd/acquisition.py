@@ -1,0 +1,99 @@
+"""Drop-in mirror of bayesopt/acquisition.py on the MI355X (same names and semantics).
+
+Arrays may be numpy (results copied back in place, as the reference mutates them) or HIP
+device tensors.
+"""
+
+from __future__ import annotations
+
+import ctypes as _C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .device import F64, Workspace, stream_handle
+from .kernels import _Arg, _dev_of, _host_vec
+
+C_i64 = _C.c_int64
+
+
+def upper_confidence_bound(mu, variance, beta):
+    """acquisition.py:33-52 — mu + beta * sqrt(|variance|) (returns a new array)."""
+    dev = _dev_of(mu, variance)
+    m = _Arg(mu, dev)
+    v = _Arg(variance, dev)
+    out = torch.empty_like(m.t)
+    _lib.check(_lib.load().bo_update_ucb(out.data_ptr(), m.ptr, v.ptr, 1, m.t.numel(),
+                                         _host_vec([beta], 1), stream_handle(dev)), "bo_update_ucb")
+    return out if isinstance(mu, torch.Tensor) else out.cpu().numpy()
+
+
+def update_ucb(ucb, mu_objectives, variance_objectives, betas):
+    """acquisition.py:55-81 — per-objective UCB, in place."""
+    dev = _dev_of(ucb, mu_objectives)
+    u = _Arg(ucb, dev, write=True)
+    m = _Arg(mu_objectives, dev)
+    v = _Arg(variance_objectives, dev)
+    n_obj, n = m.t.shape
+    _lib.check(_lib.load().bo_update_ucb(u.ptr, m.ptr, v.ptr, n_obj, n, _host_vec(betas, n_obj),
+                                         stream_handle(dev)), "bo_update_ucb")
+    u.finish()
+
+
+def update_hypervolume_improvement(acquisition_values, ucb):
+    """acquisition.py:89-108 — the reference's "HVI": sum of per-objective UCB, in place."""
+    dev = _dev_of(acquisition_values, ucb)
+    a = _Arg(acquisition_values, dev, write=True)
+    u = _Arg(ucb, dev)
+    n_obj, n = u.t.shape
+    _lib.check(_lib.load().bo_update_hypervolume_improvement(a.ptr, u.ptr, n_obj, n, stream_handle(dev)),
+               "bo_update_hypervolume_improvement")
+    a.finish()
+
+
+def select_indices(acquisition_values, cands, evaluated_points, batch_size, dev=None):
+    """Global candidate indices of select_next_batch's choice (device top-q with exclusion).
+
+    Order: NaN first, then descending value, ties by ascending index (the reference's
+    argsort tie order is unspecified).  Batches above BO_MAX_TOPQ are taken in rounds,
+    each round excluding the points already chosen.
+    """
+    dev = dev or _dev_of(acquisition_values, evaluated_points)
+    acq = _Arg(acquisition_values, dev)
+    ev = np.asarray(evaluated_points.cpu().numpy() if isinstance(evaluated_points, torch.Tensor)
+                    else evaluated_points, dtype=np.float64).reshape(-1, cands.dim)
+    lib = _lib.load()
+    chosen = []
+    while len(chosen) < batch_size:
+        q = min(_lib.MAX_TOPQ, batch_size - len(chosen))
+        excl = ev if not chosen else np.concatenate([ev, cands.points(np.array(chosen)).astype(np.float64)])
+        ex = torch.as_tensor(np.ascontiguousarray(excl), device=dev)
+        tv = torch.empty(q, dtype=F64, device=dev)
+        ti = torch.empty(q, dtype=torch.int64, device=dev)
+        lo = (C_i64 * 8)(*(list(cands.lo or []) + [0] * (8 - len(cands.lo or []))))
+        sh = (C_i64 * 8)(*(list(cands.shape or []) + [1] * (8 - len(cands.shape or []))))
+        nbytes = lib.bo_select_topq_workspace_size(cands.n, q)
+        ws = Workspace.get(nbytes, dev)
+        _lib.check(lib.bo_select_topq(acq.ptr, cands.n, cands.kind_code,
+                                      cands.tensor.data_ptr() if cands.tensor is not None else None,
+                                      lo, sh, cands.dim, 0, ex.data_ptr() if ex.numel() else None,
+                                      ex.shape[0], q, tv.data_ptr(), ti.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), stream_handle(dev)), "bo_select_topq")
+        got = [int(i) for i in ti.cpu().numpy() if i >= 0]
+        chosen.extend(got)
+        if len(got) < q:
+            break
+    return np.array(chosen, dtype=np.int64)
+
+
+def select_next_batch(input_space, acquisition_values, evaluated_points, batch_size=3):
+    """acquisition.py:116-144 — the best `batch_size` candidates (descending acquisition)
+    that are not equal to an evaluated point; returns a new array of candidate rows."""
+    from .predict import CandidateSet
+    cands = CandidateSet.explicit(input_space, _dev_of(acquisition_values, input_space))
+    idx = select_indices(acquisition_values, cands, evaluated_points, batch_size)
+    if isinstance(input_space, torch.Tensor):
+        return input_space[torch.as_tensor(idx, device=input_space.device)].cpu().numpy()
+    return np.asarray(input_space)[idx]
+

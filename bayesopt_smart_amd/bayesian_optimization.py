@@ -1,0 +1,252 @@
+"""Drop-in for bayesopt/bayesian_optimization.py: ``optimize`` and ``BayesianOptimization``
+with the reference's signatures, kwargs, ``state`` dict and return values, running the
+inner loop (bayesian_optimization.py:108-247) on the MI355X:
+
+  hyper-parameters   Powell on the host, every MLL evaluation one device call (bo_compute_mll)
+  update_k/invert_k  device kernels (bo_update_k, bo_invert_k)
+  predict+acquire    ONE fused kernel call (bo_predict_acquire) replacing update_k_star ->
+                     update_mean -> update_variance -> standardize_objectives -> update_ucb ->
+                     update_hypervolume_improvement -> select_next_batch; the N x M k_star
+                     buffer of the reference is never allocated
+  evaluation         the user's objective on the host (unchanged)
+
+Posterior arrays stay in HBM; callbacks receive a ``state`` dict whose array entries are
+copied to numpy only when a callback reads them.
+"""
+
+from __future__ import annotations
+
+import time
+from typing import Any, Callable, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .acquisition import select_indices
+from .config import (DEFAULT_BATCH_SIZE, DEFAULT_BETA, DEFAULT_INITIAL_SAMPLES,
+                     DEFAULT_LENGTH_SCALE, DEFAULT_PRIOR_MEAN, DEFAULT_PRIOR_VARIANCE,
+                     NUMBA_FLOAT_TYPE)
+from .device import F64, require_device
+from .pareto import compute_pareto_front, print_pareto_analysis
+from .predict import CandidateSet, predict_acquire
+from . import _lib
+
+
+class LazyState(dict):
+    """``state`` dict (bayesian_optimization.py:226-243); device arrays become numpy on read."""
+
+    def __getitem__(self, key):
+        v = dict.__getitem__(self, key)
+        if isinstance(v, torch.Tensor):
+            v = v.cpu().numpy()
+            dict.__setitem__(self, key, v)
+        return v
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+
+class DeviceBuffers:
+    """The reference's preallocated posterior arrays (bayesian_optimization.py:355-401), in HBM.
+    k_star (n_obj x T x M) is not among them: the fused kernel never materialises it."""
+
+    def __init__(self, n_obj, total, m, dev):
+        z = lambda *s: torch.zeros(s, dtype=F64, device=dev)  # noqa: E731
+        self.kernel_matrices = z(n_obj, total, total)
+        self.mu_objectives = z(n_obj, m)
+        self.variance_objectives = z(n_obj, m)
+        self.std_mu_objectives = z(n_obj, m)
+        self.std_variance_objectives = z(n_obj, m)
+        self.ucb = z(n_obj, m)
+        self.acquisition_values = z(m)
+
+
+def _predict_select(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
+                    buffers: DeviceBuffers, batch_size, evaluated):
+    """The fused predict + acquisition + select step; returns x_next (int64 rows)."""
+    out = {"mu": buffers.mu_objectives, "var": buffers.variance_objectives,
+           "std_mu": buffers.std_mu_objectives, "std_var": buffers.std_variance_objectives,
+           "ucb": buffers.ucb, "acq": buffers.acquisition_values}
+    q = batch_size if batch_size <= _lib.MAX_TOPQ else 0
+    r = predict_acquire(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
+                        outputs=tuple(out), topq=q, out=out)
+    if q:
+        idx = r["top_idx"].cpu().numpy()
+        idx = idx[idx >= 0]
+    else:  # batches above BO_MAX_TOPQ: rounds of the standalone device selection
+        idx = select_indices(buffers.acquisition_values, cands, evaluated, batch_size)
+    if idx.size == 0:
+        return np.zeros((0, cands.dim), dtype=np.int64)
+    return cands.points(idx)
+
+
+def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, variance_objectives,
+             std_mu_objectives, std_variance_objectives, ucb, acquisition_values, input_space,
+             prior_mean, prior_variance, reference_point, n_evaluations, total_samples,
+             n_objectives, function, betas, length_scales, batch_size, bounds,
+             callbacks: Optional[List[Callable]] = None) -> Tuple[np.ndarray, np.ndarray, int]:
+    """bayesian_optimization.py:51-247 with the reference's argument list.
+
+    `kernel_matrices` and the posterior arrays may be HIP tensors (in place) or numpy arrays;
+    `k_star` is accepted for signature compatibility and not used (nothing N x M is
+    materialised); `input_space` may be a CandidateSet, a device tensor or the reference's
+    int64 numpy array.  Returns (x_vector, y_vector, last_eval + 1) like the reference
+    (including its count quirk, :247).
+    """
+    dev = require_device()
+    del k_star, reference_point, n_objectives, bounds  # unused, as in the reference
+    cands = input_space if isinstance(input_space, CandidateSet) else CandidateSet.explicit(input_space, dev)
+    n_obj = len(prior_mean)
+
+    def dev_buf(a, shape):
+        if isinstance(a, torch.Tensor) and a.device.type == "cuda":
+            return a
+        return torch.zeros(shape, dtype=F64, device=dev)
+
+    m = cands.n
+    bufs = DeviceBuffers.__new__(DeviceBuffers)
+    bufs.kernel_matrices = dev_buf(kernel_matrices, (n_obj, total_samples, total_samples))
+    bufs.mu_objectives = dev_buf(mu_objectives, (n_obj, m))
+    bufs.variance_objectives = dev_buf(variance_objectives, (n_obj, m))
+    bufs.std_mu_objectives = dev_buf(std_mu_objectives, (n_obj, m))
+    bufs.std_variance_objectives = dev_buf(std_variance_objectives, (n_obj, m))
+    bufs.ucb = dev_buf(ucb, (n_obj, m))
+    bufs.acquisition_values = dev_buf(acquisition_values, (m,))
+
+    last_eval = 0
+    for current_eval in range(n_evaluations, total_samples, batch_size):
+        iter_start = time.perf_counter()
+        t0 = time.perf_counter()
+        xd = torch.as_tensor(np.ascontiguousarray(x_vector[:current_eval], dtype=np.float64), device=dev)
+        yd = torch.as_tensor(np.ascontiguousarray(y_vector[:current_eval], dtype=np.float64), device=dev)
+        optimized = K.optimize_hyperparams_mll(xd, yd, bufs.kernel_matrices, prior_mean, prior_variance,
+                                               length_scales, current_eval)
+        t1 = time.perf_counter()
+        K.update_k(bufs.kernel_matrices, xd, 0, current_eval, prior_variance, length_scales)
+        kinv = K.invert_k(current_eval, bufs.kernel_matrices)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        x_next = _predict_select(xd, yd, kinv, cands, prior_mean, prior_variance, length_scales, betas,
+                                 bufs, batch_size, x_vector[:current_eval])
+        t3 = time.perf_counter()
+        for b_idx, point in enumerate(x_next):
+            x_vector[current_eval + b_idx] = point
+            y_vector[current_eval + b_idx] = function(point)
+        last_eval = current_eval
+        t4 = time.perf_counter()
+        if callbacks:
+            state = LazyState({
+                "iteration": current_eval,
+                "n_evaluations": current_eval + batch_size,
+                "x_vector": x_vector[: current_eval + batch_size],
+                "y_vector": y_vector[: current_eval + batch_size],
+                "mu_objectives": bufs.mu_objectives,
+                "variance_objectives": bufs.variance_objectives,
+                "acquisition_values": bufs.acquisition_values,
+                "x_next": x_next,
+                "hyperparams": optimized.x,
+                "timings": {"hyperparams": t1 - t0, "kernels": t2 - t1, "acquisition": t3 - t2,
+                            "eval": t4 - t3, "total": t4 - iter_start},
+            })
+            for cb in callbacks:
+                cb(state)
+    for name, a in (("mu", mu_objectives), ("var", variance_objectives), ("smu", std_mu_objectives),
+                    ("svar", std_variance_objectives), ("ucb", ucb), ("acq", acquisition_values)):
+        if isinstance(a, np.ndarray):   # numpy callers get their arrays filled, as in the reference
+            src = {"mu": bufs.mu_objectives, "var": bufs.variance_objectives,
+                   "smu": bufs.std_mu_objectives, "svar": bufs.std_variance_objectives,
+                   "ucb": bufs.ucb, "acq": bufs.acquisition_values}[name]
+            a[...] = src.cpu().numpy()
+    return x_vector, y_vector, last_eval + 1
+
+
+class BayesianOptimization:
+    """bayesian_optimization.py:250-488 — same constructor, kwargs and methods.
+
+    Extra kwargs (not in the reference): ``input_space`` (explicit [M, d] candidates, e.g.
+    a Sobol set, instead of the integer grid) and ``device``.
+    """
+
+    def __init__(self, function: Callable[[np.ndarray], np.ndarray], bounds: List[Tuple[int, int]],
+                 n_objectives: int = 3, n_iterations: int = 10, **kwargs: Any):
+        self.device = require_device(kwargs.get("device"))
+        self.function = function
+        self.bounds = bounds
+        self.n_objectives = n_objectives
+        self.n_iterations = n_iterations
+        cb = kwargs.get("callbacks", None)
+        self.callbacks = [] if cb is None else (cb if isinstance(cb, list) else [cb])
+        self.prior_mean = np.array(kwargs.get("prior_mean", [DEFAULT_PRIOR_MEAN] * n_objectives),
+                                   dtype=NUMBA_FLOAT_TYPE)
+        self.prior_variance = np.array(kwargs.get("prior_variance", [DEFAULT_PRIOR_VARIANCE] * n_objectives),
+                                       dtype=NUMBA_FLOAT_TYPE)
+        self.length_scales = np.array(kwargs.get("length_scales", [DEFAULT_LENGTH_SCALE] * n_objectives),
+                                      dtype=NUMBA_FLOAT_TYPE)
+        self.betas = np.array(kwargs.get("betas", [DEFAULT_BETA] * n_objectives), dtype=NUMBA_FLOAT_TYPE)
+        self.batch_size = kwargs.get("batch_size", DEFAULT_BATCH_SIZE)
+        self.initial_samples = kwargs.get("initial_samples", DEFAULT_INITIAL_SAMPLES)
+        self.dim = len(bounds)
+        explicit = kwargs.get("input_space")
+        self.candidates = (CandidateSet.grid(bounds) if explicit is None
+                           else CandidateSet.explicit(explicit, self.device))
+        self._input_space = None
+        self.total_samples = self.initial_samples + self.n_iterations * self.batch_size
+        self.x_vector = np.zeros((self.total_samples, self.dim), dtype=NUMBA_FLOAT_TYPE)
+        self.y_vector = np.zeros((self.total_samples, n_objectives), dtype=NUMBA_FLOAT_TYPE)
+        self._buffers = DeviceBuffers(n_objectives, self.total_samples, self.candidates.n, self.device)
+        self.k_star = None   # never materialised (the reference allocates n_obj x T x M here)
+        self.n_evaluations = K.initialize_lhs_integer(self.x_vector, self.y_vector,
+                                                      np.array(self.bounds, dtype=np.int64),
+                                                      self.function, self.initial_samples)
+        if np.all(self.prior_mean == DEFAULT_PRIOR_MEAN):
+            self.prior_mean = K.compute_prior_mean(self.y_vector, self.n_evaluations, n_objectives)
+        if np.all(self.prior_variance == DEFAULT_PRIOR_VARIANCE):
+            self.prior_variance = K.compute_prior_variance(self.y_vector, self.n_evaluations, n_objectives)
+        self.reference_point = np.array([0.0] * n_objectives)
+
+    # the reference's preallocated arrays, materialised on the host on demand
+    @property
+    def input_space(self):
+        if self._input_space is None:
+            self._input_space = self.candidates.materialize(self.device).cpu().numpy()
+        return self._input_space
+
+    def _np(self, name):
+        return getattr(self._buffers, name).cpu().numpy()
+
+    kernel_matrices = property(lambda self: self._np("kernel_matrices"))
+    mu_objectives = property(lambda self: self._np("mu_objectives"))
+    variance_objectives = property(lambda self: self._np("variance_objectives"))
+    std_mu_objectives = property(lambda self: self._np("std_mu_objectives"))
+    std_variance_objectives = property(lambda self: self._np("std_variance_objectives"))
+    ucb = property(lambda self: self._np("ucb"))
+    acquisition_values = property(lambda self: self._np("acquisition_values"))
+
+    def optimize(self) -> None:
+        """bayesian_optimization.py:427-463."""
+        b = self._buffers
+        self.x_vector, self.y_vector, self.n_evaluations = optimize(
+            x_vector=self.x_vector, y_vector=self.y_vector, kernel_matrices=b.kernel_matrices,
+            k_star=None, mu_objectives=b.mu_objectives, variance_objectives=b.variance_objectives,
+            std_mu_objectives=b.std_mu_objectives, std_variance_objectives=b.std_variance_objectives,
+            ucb=b.ucb, acquisition_values=b.acquisition_values, input_space=self.candidates,
+            prior_mean=self.prior_mean, prior_variance=self.prior_variance,
+            reference_point=self.reference_point, n_evaluations=self.n_evaluations,
+            total_samples=self.total_samples, n_objectives=self.n_objectives, function=self.function,
+            betas=self.betas, length_scales=self.length_scales, batch_size=self.batch_size,
+            bounds=self.bounds, callbacks=self.callbacks if self.callbacks else None)
+
+    def pareto_analysis(self) -> np.ndarray:
+        """bayesian_optimization.py:465-488."""
+        ey = self.y_vector[: self.n_evaluations]
+        ex = self.x_vector[: self.n_evaluations]
+        px, py = compute_pareto_front(ex, ey)
+        print_pareto_analysis(px, py)
+        return py

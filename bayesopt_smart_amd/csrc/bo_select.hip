@@ -79,6 +79,25 @@ __global__ void std_ucb_hvi_kernel(double* __restrict__ smu, double* __restrict_
   if (acq) acq[i] = a;
 }
 
+__global__ void ucb_kernel(double* __restrict__ ucb, const double* __restrict__ mu,
+                           const double* __restrict__ var, int n_obj, long long n, HostParams p) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int o = 0; o < n_obj; ++o) {
+    const long long off = (long long)o * n + i;
+    ucb[off] = mu[off] + p.a[o] * sqrt(fabs(var[off]));
+  }
+}
+
+__global__ void hvi_kernel(double* __restrict__ acq, const double* __restrict__ ucb, int n_obj,
+                           long long n) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double a = ucb[i];
+  for (int o = 1; o < n_obj; ++o) a += ucb[(long long)o * n + i];
+  acq[i] = a;
+}
+
 // ------------------------------------------------------------------------ selection
 struct SelArgs {
   const double* acq;
@@ -271,6 +290,29 @@ int bo_standardize_ucb_hvi(double* smu, double* svar, double* ucb, double* acq, 
   }
   hipLaunchKernelGGL(std_ucb_hvi_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, smu, svar, ucb, acq, mu, var, n_obj, (long long)n, p, q);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+int bo_update_ucb(double* ucb, const double* mu, const double* var, int32_t n_obj, int64_t n,
+                  const double* betas, void* stream) {
+  if (!ucb || !mu || !var || !betas || n_obj < 1 || n_obj > BO_MAX_OBJ || n < 0) return BO_ERR_ARG;
+  if (n == 0) return BO_OK;
+  HostParams p;
+  memset(&p, 0, sizeof(p));
+  for (int o = 0; o < n_obj; ++o) p.a[o] = betas[o];
+  hipLaunchKernelGGL(ucb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, ucb, mu, var, n_obj, (long long)n, p);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+int bo_update_hypervolume_improvement(double* acq, const double* ucb, int32_t n_obj, int64_t n,
+                                      void* stream) {
+  if (!acq || !ucb || n_obj < 1 || n < 0) return BO_ERR_ARG;
+  if (n == 0) return BO_OK;
+  hipLaunchKernelGGL(hvi_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, acq, ucb, n_obj, (long long)n);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
 }

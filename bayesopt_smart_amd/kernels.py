@@ -1,0 +1,271 @@
+"""Drop-in mirror of bayesopt/numba_kernels.py on the MI355X.
+
+Same names, argument meaning, in-place conventions and error behaviour as the reference
+functions; the arithmetic runs in libbo_amd.so kernels.  Arrays may be numpy arrays (as the
+reference passes them: results are copied back in place) or HIP device tensors (no host
+round trip).  Only the hyper-parameter optimiser driver (scipy Powell, a sequential host
+algorithm) and the initial LHS design stay on the host, as SURVEY.md §2 scopes them.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+from scipy.optimize import minimize
+
+from . import _lib
+from .config import (HYPERPARAM_FTOL, HYPERPARAM_MAXITER, HYPERPARAM_METHOD,
+                     HYPERPARAM_MIN_BOUND, HYPERPARAM_XTOL, NUMBA_FLOAT_TYPE)
+from .device import F64, Workspace, require_device, stream_handle
+
+
+# ------------------------------------------------------------------------ helpers
+class _Arg:
+    """A caller array on the device; numpy inputs are staged and (if written) copied back."""
+
+    def __init__(self, arr, dev, dtype=F64, write=False):
+        self.src = arr
+        self.write = write
+        if isinstance(arr, torch.Tensor):
+            if arr.device.type != "cuda" or arr.dtype != dtype or not arr.is_contiguous():
+                raise ValueError("device arrays must be contiguous HIP tensors of the right dtype")
+            self.t = arr
+            self.host = False
+        else:
+            a = np.asarray(arr)
+            self.t = torch.as_tensor(np.ascontiguousarray(a, dtype=torch_to_np(dtype)), device=dev)
+            self.host = True
+
+    @property
+    def ptr(self):
+        return self.t.data_ptr()
+
+    def finish(self):
+        if self.write and self.host:
+            torch.cuda.current_stream(self.t.device).synchronize()
+            self.src[...] = self.t.cpu().numpy().reshape(np.shape(self.src))
+
+
+def torch_to_np(dtype):
+    return {torch.float64: np.float64, torch.int64: np.int64, torch.uint8: np.uint8}[dtype]
+
+
+def _host_vec(v, n):
+    a = np.asarray(v.cpu().numpy() if isinstance(v, torch.Tensor) else v, dtype=np.float64).ravel()
+    if a.size < n:
+        raise ValueError("per-objective parameter array too short")
+    return (C.c_double * max(n, 1))(*[float(x) for x in a[:n]])
+
+
+def _dev_of(*arrs):
+    for a in arrs:
+        if isinstance(a, torch.Tensor) and a.device.type == "cuda":
+            return a.device
+    return require_device()
+
+
+# ----------------------------------------------------------------------- init/prior
+def initialize_lhs_integer(x_vector, y_vector, bounds, function, n_samples=8):
+    """numba_kernels.py:50-95 — integer Latin hypercube (numpy global RNG, same draw order
+    as the reference's debug mode); evaluates `function` on the host."""
+    bounds = np.asarray(bounds)
+    dim = len(bounds)
+    samples = np.empty((n_samples, dim), dtype=NUMBA_FLOAT_TYPE)
+    for d in range(dim):
+        perm = np.random.permutation(n_samples)
+        lo, hi = bounds[d, 0], bounds[d, 1]
+        step = (hi - lo) / n_samples
+        for i in range(n_samples):
+            low = lo + perm[i] * step
+            high = lo + (perm[i] + 1) * step
+            samples[i, d] = min(int(np.random.uniform(low, high)), hi - 1)
+    for i in range(n_samples):
+        x_vector[i] = samples[i]
+        y_vector[i] = function(x_vector[i])
+    return n_samples
+
+
+def compute_prior_mean(y_vector, n_evaluations, n_objectives):
+    """numba_kernels.py:103-122 (O(N) host statistic of the initial design)."""
+    y = y_vector.cpu().numpy() if isinstance(y_vector, torch.Tensor) else np.asarray(y_vector)
+    return np.array([np.mean(y[:n_evaluations, o]) for o in range(n_objectives)], dtype=np.float64)
+
+
+def compute_prior_variance(y_vector, n_evaluations, n_objectives):
+    """numba_kernels.py:125-144 (population variance)."""
+    y = y_vector.cpu().numpy() if isinstance(y_vector, torch.Tensor) else np.asarray(y_vector)
+    return np.array([np.var(y[:n_evaluations, o]) for o in range(n_objectives)], dtype=np.float64)
+
+
+# --------------------------------------------------------------------------- GP fit
+def update_k(kernel_matrix, x_vector, last_eval, current_eval, prior_variance, length_scales):
+    """numba_kernels.py:329-367 — RBF Gram rows [last_eval, current_eval) (+ mirror)."""
+    dev = _dev_of(kernel_matrix, x_vector)
+    km = _Arg(kernel_matrix, dev, write=True)
+    x = _Arg(x_vector, dev)
+    n_obj, ld = km.t.shape[0], km.t.shape[-1]
+    lib = _lib.load()
+    _lib.check(lib.bo_update_k(km.ptr, ld, n_obj, x.ptr, x.t.shape[1], int(last_eval), int(current_eval),
+                               _host_vec(prior_variance, n_obj), _host_vec(length_scales, n_obj),
+                               stream_handle(dev)), "bo_update_k")
+    km.finish()
+
+
+def invert_k(current_eval, kernel_matrix):
+    """numba_kernels.py:370-403 — inv(K[:N,:N] + 1e-6 I) per objective (LU-class pivoting).
+
+    Returns a new array of the caller's kind (numpy in, numpy out; tensor in, tensor out).
+    Raises numpy.linalg.LinAlgError on an exactly singular pivot.
+    """
+    dev = _dev_of(kernel_matrix)
+    km = _Arg(kernel_matrix, dev)
+    n_obj, ld = km.t.shape[0], km.t.shape[-1]
+    n = int(current_eval)
+    out = torch.empty((n_obj, n, n), dtype=F64, device=dev)
+    lib = _lib.load()
+    ws = Workspace.get(lib.bo_invert_k_workspace_size(n_obj, n), dev)
+    _lib.check(lib.bo_invert_k(out.data_ptr(), km.ptr, ld, n_obj, n, ws.data_ptr(), ws.numel(),
+                               stream_handle(dev)), "bo_invert_k")
+    return out if isinstance(kernel_matrix, torch.Tensor) else out.cpu().numpy()
+
+
+def compute_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance, length_scales,
+                current_eval):
+    """numba_kernels.py:152-235 — summed marginal log likelihood (Gram rebuilt in place).
+
+    Raises numpy.linalg.LinAlgError when K/pv + 1e-8 I is not positive definite (:214).
+    """
+    dev = _dev_of(kernel_matrix, x_vector, y_vector)
+    km = _Arg(kernel_matrix, dev, write=True)
+    x = _Arg(x_vector, dev)
+    y = _Arg(y_vector, dev)
+    n_obj, ld = km.t.shape[0], km.t.shape[-1]
+    n = int(current_eval)
+    lib = _lib.load()
+    ws = Workspace.get(lib.bo_compute_mll_workspace_size(n_obj, n), dev)
+    out = C.c_double()
+    st = lib.bo_compute_mll(C.byref(out), x.ptr, x.t.shape[1], y.ptr, y.t.stride(0), km.ptr, ld, n_obj,
+                            _host_vec(prior_mean, n_obj), _host_vec(prior_variance, n_obj),
+                            _host_vec(length_scales, n_obj), n, ws.data_ptr(), ws.numel(),
+                            stream_handle(dev))
+    km.finish()
+    _lib.check(st, "bo_compute_mll")
+    return out.value
+
+
+def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance,
+                             length_scales, current_eval):
+    """numba_kernels.py:238-321 — Powell over [ls..., var...] (bounds >= 1e-5) maximising the
+    device MLL; updates length_scales and prior_variance in place, returns the OptimizeResult.
+    The training arrays are staged on the device once for all ~100-200 MLL evaluations."""
+    dev = _dev_of(kernel_matrix, x_vector, y_vector)
+    n_obj = np.asarray(length_scales).shape[0] if not isinstance(length_scales, torch.Tensor) \
+        else length_scales.shape[0]
+    xd = _Arg(x_vector, dev).t
+    yd = _Arg(y_vector, dev).t
+    km = _Arg(kernel_matrix, dev, write=True)
+    ls0 = length_scales.cpu().numpy() if isinstance(length_scales, torch.Tensor) else np.asarray(length_scales)
+    pv0 = prior_variance.cpu().numpy() if isinstance(prior_variance, torch.Tensor) else np.asarray(prior_variance)
+    initial_guess = np.concatenate([ls0, pv0])
+    bounds = [(HYPERPARAM_MIN_BOUND, None)] * (2 * n_obj)
+
+    def objective(params):
+        return -compute_mll(xd, yd, km.t, prior_mean, params[n_obj:], params[:n_obj], current_eval)
+
+    res = minimize(objective, initial_guess, method=HYPERPARAM_METHOD, bounds=bounds,
+                   options={"xtol": HYPERPARAM_XTOL, "ftol": HYPERPARAM_FTOL,
+                            "maxiter": HYPERPARAM_MAXITER})
+    km.finish()
+    _assign(length_scales, res.x[:n_obj])
+    _assign(prior_variance, res.x[n_obj:])
+    return res
+
+
+def _assign(dst, values):
+    if isinstance(dst, torch.Tensor):
+        dst.copy_(torch.as_tensor(values, dtype=dst.dtype))
+    else:
+        dst[:] = values
+
+
+# ----------------------------------------------------------------------- GP predict
+def _cand_kind(t):
+    return _lib.CAND_I64 if t.dtype == torch.int64 else _lib.CAND_F64
+
+
+def update_k_star(k_star, x_vector, input_space, last_eval, current_eval, prior_variance,
+                  length_scales):
+    """numba_kernels.py:406-442 — materialised k_star[o, e, i] rows [last_eval, current_eval).
+    (The fused path, predict.predict_acquire, never materialises it.)"""
+    dev = _dev_of(k_star, x_vector, input_space)
+    ks = _Arg(k_star, dev, write=True)
+    x = _Arg(x_vector, dev)
+    is_int = (not input_space.is_floating_point()) if isinstance(input_space, torch.Tensor) \
+        else np.issubdtype(np.asarray(input_space).dtype, np.integer)
+    cand = _Arg(input_space, dev, dtype=torch.int64 if is_int else F64)
+    n_obj, ld_rows, m = ks.t.shape
+    lib = _lib.load()
+    _lib.check(lib.bo_update_k_star(ks.ptr, ld_rows, n_obj, x.ptr, x.t.shape[1], _cand_kind(cand.t),
+                                    cand.ptr, m, int(last_eval), int(current_eval),
+                                    _host_vec(prior_variance, n_obj), _host_vec(length_scales, n_obj),
+                                    stream_handle(dev)), "bo_update_k_star")
+    ks.finish()
+
+
+def _mean_variance(mu_objectives, variance_objectives, k_star, kinv, y_vector, prior_mean,
+                   prior_variance, current_eval):
+    dev = _dev_of(k_star, kinv, mu_objectives, variance_objectives)
+    ks = _Arg(k_star, dev)
+    ki = _Arg(kinv, dev)
+    n_obj, ld_rows, m = ks.t.shape
+    n = int(current_eval)
+    mu = _Arg(mu_objectives, dev, write=True) if mu_objectives is not None else None
+    var = _Arg(variance_objectives, dev, write=True) if variance_objectives is not None else None
+    if y_vector is None:
+        y = torch.zeros((n, n_obj), dtype=F64, device=dev)
+    else:
+        y = _Arg(y_vector, dev).t
+    pm = prior_mean if prior_mean is not None else np.zeros(n_obj)
+    pv = prior_variance if prior_variance is not None else np.ones(n_obj)
+    lib = _lib.load()
+    ws = Workspace.get(lib.bo_update_mean_variance_workspace_size(n_obj, n), dev)
+    _lib.check(lib.bo_update_mean_variance(mu.ptr if mu else None, var.ptr if var else None, ks.ptr,
+                                           ld_rows, n_obj, m, ki.ptr, ki.t.shape[-1], y.data_ptr(),
+                                           y.stride(0), n, _host_vec(pm, n_obj), _host_vec(pv, n_obj),
+                                           ws.data_ptr(), ws.numel(), stream_handle(dev)),
+               "bo_update_mean_variance")
+    for a in (mu, var):
+        if a is not None:
+            a.finish()
+
+
+def update_mean(mu_objectives, k_star, inverted_kernel_matrix, y_vector, prior_mean, current_eval):
+    """numba_kernels.py:450-488 — mu = pm + K*^T (Kinv (y - pm))."""
+    _mean_variance(mu_objectives, None, k_star, inverted_kernel_matrix, y_vector, prior_mean, None,
+                   current_eval)
+
+
+def update_variance(variance_objectives, k_star, inverted_kernel_matrix, prior_variance, current_eval):
+    """numba_kernels.py:491-535 — var = max(pv - sum_e K* (Kinv K*), 1e-10)."""
+    _mean_variance(None, variance_objectives, k_star, inverted_kernel_matrix, None, None,
+                   prior_variance, current_eval)
+
+
+def standardize_objectives(std_mu_objectives, std_variance_objectives, mu_objectives,
+                           variance_objectives, prior_mean, prior_variance):
+    """numba_kernels.py:538-570."""
+    dev = _dev_of(std_mu_objectives, mu_objectives)
+    smu = _Arg(std_mu_objectives, dev, write=True)
+    svar = _Arg(std_variance_objectives, dev, write=True)
+    mu = _Arg(mu_objectives, dev)
+    var = _Arg(variance_objectives, dev)
+    n_obj, m = mu.t.shape
+    lib = _lib.load()
+    zeros = _host_vec(np.zeros(n_obj), n_obj)
+    _lib.check(lib.bo_standardize_ucb_hvi(smu.ptr, svar.ptr, None, None, mu.ptr, var.ptr, n_obj, m,
+                                          _host_vec(prior_mean, n_obj), _host_vec(prior_variance, n_obj),
+                                          zeros, stream_handle(dev)), "bo_standardize_ucb_hvi")
+    smu.finish()
+    svar.finish()

@@ -143,6 +143,15 @@ int bo_standardize_ucb_hvi(double* std_mu, double* std_var, double* ucb, double*
                            const double* prior_mean, const double* prior_variance,
                            const double* betas, void* stream);
 
+/* update_ucb  bayesopt/acquisition.py:55-81: ucb[o][i] = mu[o][i] + betas[o] sqrt(|var[o][i]|)
+ * (arrays [n_obj][n]; betas host). */
+int bo_update_ucb(double* ucb, const double* mu, const double* var, int32_t n_obj, int64_t n,
+                  const double* betas, void* stream);
+
+/* update_hypervolume_improvement  bayesopt/acquisition.py:89-108: acq[i] = sum_o ucb[o][i]. */
+int bo_update_hypervolume_improvement(double* acq, const double* ucb, int32_t n_obj, int64_t n,
+                                      void* stream);
+
 /* select_next_batch  bayesopt/acquisition.py:116-144 over an acquisition array:
  * top-q (q <= BO_MAX_TOPQ) skipping candidates equal to any evaluated point. */
 int bo_select_topq(const double* acq, int64_t n_cand, int32_t cand_kind, const void* cand,

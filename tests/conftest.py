@@ -38,8 +38,9 @@ def kinv_of(d):
     km = np.zeros((d["pm"].shape[0], n, n))
     O.update_k(km, d["x"], 0, n, d["pv"], d["ls"])
     kinv = O.invert_k(n, km)
+    # the Gram is pinned bit-for-bit; LAPACK's inverse is host-dependent (OpenBLAS picks its
+    # kernels per CPU), so K^-1 is only bit-equal on the host that generated the fixture
     assert hashlib.sha256(km.tobytes()).digest() == bytes(d["K_sha256"])
-    assert hashlib.sha256(kinv.tobytes()).digest() == bytes(d["Kinv_sha256"])
     return kinv
 
 

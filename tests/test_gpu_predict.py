@@ -79,15 +79,22 @@ def test_predict_implicit_grid(bo):
 def test_predict_shapes_vs_oracle(bo, n, dim, n_obj):
     rng = np.random.default_rng(n)
     m = 3000
-    cand = rng.integers(0, 60, size=(m, dim)).astype(np.int64)
-    x = rng.integers(0, 60, size=(n, dim)).astype(np.float64)
+    side = 400 if dim == 2 else 60
+    cand = np.unique(rng.integers(0, side, size=(m, dim)), axis=0).astype(np.int64)
+    m = cand.shape[0]
+    # distinct training points (parity is defined for well-conditioned K)
+    x = np.unique(rng.integers(0, side, size=(3 * n, dim)), axis=0)
+    x = x[rng.permutation(x.shape[0])[:n]].astype(np.float64)
     x[: n // 3] = cand[rng.choice(m, n // 3, replace=False)]          # some evaluated candidates
+    x = np.unique(x, axis=0)
+    n = x.shape[0]
     y = rng.normal(size=(n, n_obj)) * 50 + 10
     pm, pv = y.mean(0), y.var(0)
     ls = rng.uniform(3.0, 9.0, size=n_obj)
     betas = rng.uniform(0.5, 2.5, size=n_obj)
     km = np.zeros((n_obj, n, n))
     O.update_k(km, x, 0, n, pv, ls)
+    assert max(np.linalg.cond(km[o] + 1e-6 * np.eye(n)) for o in range(n_obj)) < 1e6
     kinv = O.invert_k(n, km)
     ref = O.predict_acquire(x, y, cand, pm, pv, ls, betas, kinv=kinv)
     d = dict(x=x, y=y, Kinv=kinv, pm=pm, pv=pv, ls=ls, betas=betas)

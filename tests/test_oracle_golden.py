@@ -4,6 +4,8 @@ The fixtures come from tests/golden/make_golden.py (reference imported in its de
 mode).  Where the arithmetic order is the same the oracle must match bit-for-bit;
 the exp/LAPACK-dependent outputs are allowed 1-ulp-class differences.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -22,7 +24,10 @@ def test_gram_and_inverse(golden, name):
     d = golden(name)
     n = d["x"].shape[0]
     if "K" not in d.files:
-        kinv_of(d)      # recomputes and checks both sha256 digests of the reference's bytes
+        import hashlib
+        kinv = kinv_of(d)   # recomputes the Gram and checks its sha256 against the reference's
+        if os.path.exists("/root/reference"):   # the fixture's host: LAPACK inverse bit-equal too
+            assert hashlib.sha256(kinv.tobytes()).digest() == bytes(d["Kinv_sha256"])
         return
     km = np.zeros((d["K"].shape[0], n, n))
     O.update_k(km, d["x"], 0, n, d["pv"], d["ls"])
