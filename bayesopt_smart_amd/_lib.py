@@ -22,6 +22,7 @@ MAX_TOPQ = 48
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_WORKSPACE, ERR_HIP, ERR_NOT_PD, ERR_SINGULAR = range(7)
 CAND_I64, CAND_F64, CAND_GRID = 0, 1, 2
+MODE_AUTO, MODE_DENSE = 0, 1
 
 c_dbl_p = C.POINTER(C.c_double)
 c_vp = C.c_void_p
@@ -40,7 +41,7 @@ class PredictDesc(C.Structure):
         ("n_obj", C.c_int32), ("dim", C.c_int32), ("n_train", C.c_int64),
         ("x_train", c_vp), ("y_train", c_vp), ("ld_y", C.c_int64),
         ("kinv", c_vp), ("ld_k", C.c_int64),
-        ("cand_kind", C.c_int32), ("reserved0", C.c_int32),
+        ("cand_kind", C.c_int32), ("mode", C.c_int32),
         ("cand", c_vp), ("n_cand", C.c_int64), ("cand_offset", C.c_int64),
         ("grid_lo", C.c_int64 * MAX_DIM), ("grid_shape", C.c_int64 * MAX_DIM),
         ("excl_points", c_vp), ("n_excl", C.c_int64),

@@ -335,6 +335,20 @@ inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+// Blocked lower Cholesky, in place, of n_obj dense n x n matrices (lower triangle read and
+// written); any non-positive pivot sets *d_status = 1.  Asynchronous (no host sync).
+__attribute__((visibility("hidden"))) int bo_internal_potrf(double* C, int n, int n_obj,
+                                                            int* d_status, hipStream_t s) {
+  const int nb = (n + NB - 1) / NB;
+  for (int kb = 0; kb < nb; ++kb) {
+    hipLaunchKernelGGL(potrf_trsm_kernel, dim3(nb - kb, n_obj), dim3(256), 0, s, C, n, kb, d_status);
+    const int m = nb - kb - 1;
+    if (m > 0)
+      hipLaunchKernelGGL(syrk_kernel, dim3(m * (m + 1) / 2, n_obj), dim3(256), 0, s, C, n, kb, nb);
+  }
+  return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
+}
+
 extern "C" {
 
 size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n) {
@@ -426,14 +440,8 @@ int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* 
   hipLaunchKernelGGL(corr_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, C, km,
                      (long long)ld, (int)n, n_obj, p);
   BO_CHECK_HIP(hipGetLastError());
-  const int nb = (int)((n + NB - 1) / NB);
-  for (int kb = 0; kb < nb; ++kb) {
-    hipLaunchKernelGGL(potrf_trsm_kernel, dim3(nb - kb, n_obj), dim3(256), 0, s, C, (int)n, kb, status);
-    const int m = nb - kb - 1;
-    if (m > 0)
-      hipLaunchKernelGGL(syrk_kernel, dim3(m * (m + 1) / 2, n_obj), dim3(256), 0, s, C, (int)n, kb, nb);
-  }
-  BO_CHECK_HIP(hipGetLastError());
+  st = bo_internal_potrf(C, (int)n, n_obj, status, s);
+  if (st != BO_OK) return st;
   hipLaunchKernelGGL(mll_solve_kernel, dim3(n_obj), dim3(1024), 0, s, C, y, (long long)ld_y, (int)n,
                      p, work, dmll);
   BO_CHECK_HIP(hipGetLastError());

@@ -55,6 +55,7 @@ struct FusedArgs {
   TopEntry* partial;                     // [gridDim.x * kWaves][topq]
   const double* kstar;                   // KMEM: materialised k_star [n_obj][ks_rows][n_cand]
   long long ks_rows;
+  const int* tri_flag;                   // device: 0 => K^-1 = R R^T factored, use R^T (triangular)
 };
 
 template <int DIM>
@@ -115,50 +116,67 @@ __device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff
   return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-// One panel's contraction for E-blocks (2*ep, 2*ep+1): acc0/acc1 += W[E, panel] . B.
-// The packed stream of a panel is ordered (ep, pair, which, lane): every load is one
-// contiguous 1 KiB wave-row at scalar offset `base + ((ep*NPAIR + pair)*2 + which) KiB`.
-// The prefetch ring (kPF pairs deep) carries across ep boundaries; the caller primes it.
-template <int NS, bool SELECT>
-__device__ __forceinline__ void panel_epair(__amdgpu_buffer_rsrc_t wr, int voff, int base,
-                                            int ep, const double (&B)[NS],
-                                            d2 (&wa)[kPF], d2 (&wb)[kPF], d4& acc0, d4& acc1,
-                                            double (&sel0)[4], double (&sel1)[4]) {
-  constexpr int NPAIR = NS / 2;
-  const int so0 = base + ((ep * NPAIR * 2) << 10);
+// One E-pair (E = 2ep, 2ep+1: 32 training rows) of one panel: acc0/acc1 += W[E, panel] . B.
+// The k-steps are walked in chunks of 8 (4 pairs, 32 rows); a chunk's 4 pairs use ring
+// slots 0..3, so every E-pair starts at slot 0 and the ring index stays static.
+// The packed stream is consumed strictly in order: `pos` counts pairs (2 KiB each: the A
+// fragments of E and E+1) and the load for pair pos+4 refills the slot just consumed.
+// Past the end of the stream the buffer range check returns zeros (no fault, no branch).
+//   dense (tri = false): every chunk; K*[e][j] for the epilogue is selected from B by
+//     masked FMAs (chunk c == ep holds rows 32ep .. 32ep+31).
+//   triangular (tri = true): W = R^T is upper triangular, so E-pair ep needs chunks c >= ep
+//     only (about half the MFMAs); the epilogue is |v|^2 and needs no selection.
+// Multi-panel (N > 512, RECOMP): the epilogue rows of E-pair ep+1 are recomputed (8 exps per
+// lane), one per chunk during E-pair ep's MFMAs, so that VALU work issues in the matrix-core
+// shadow instead of serialising after the contraction.
+template <int NS, int DIM, bool SELECT, bool RECOMP>
+__device__ __forceinline__ void contract_epair(__amdgpu_buffer_rsrc_t wr, int voff, int base,
+                                               int& pos, int ep, bool tri, const double (&B)[NS],
+                                               d2 (&wa)[kPF], d2 (&wb)[kPF], d4& acc0, d4& acc1,
+                                               double (&sel0)[4], double (&sel1)[4],
+                                               const double* xs, const double (&cc)[DIM],
+                                               double pv, double nhl, int g, double (&nxt)[8]) {
+  constexpr int NCH = NS / 8;
 #pragma unroll
-  for (int p = 0; p < NPAIR; ++p) {
-    const d2 ca = wa[p % kPF];
-    const d2 cb = wb[p % kPF];
-    // prefetch kPF pairs ahead; past the end of the stream the buffer range check
-    // returns zeros (no fault), so the load needs no condition
-    wa[p % kPF] = wload(wr, voff, so0 + (((p + kPF) * 2) << 10));
-    wb[p % kPF] = wload(wr, voff, so0 + (((p + kPF) * 2 + 1) << 10));
-    acc0 = mfma64(ca.x, B[2 * p], acc0);
-    acc1 = mfma64(cb.x, B[2 * p], acc1);
-    acc0 = mfma64(ca.y, B[2 * p + 1], acc0);
-    acc1 = mfma64(cb.y, B[2 * p + 1], acc1);
-    if (SELECT && (p & 1) == 1) {
-      const int c = p >> 1;  // chunk of 4 k-steps = rows 16c..16c+15
-      const double m0 = (c == 2 * ep) ? 1.0 : 0.0, m1 = (c == 2 * ep + 1) ? 1.0 : 0.0;
+  for (int c = 0; c < NCH; ++c) {
+    if (RECOMP && c < 8) {
+      // row of E-pair ep+1 for slot c: e = 32(ep+1) + 16(c>>2) + g + 4(c&3)
+      const int e = 32 * (ep + 1) + 16 * (c >> 2) + g + 4 * (c & 3);
+      nxt[c] = pv * exp(sqdist<DIM>(xs, e, cc) * nhl);
+    }
+    if (!tri || c >= ep) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sel0[r] = __builtin_fma(m0, B[4 * c + r], sel0[r]);
-        sel1[r] = __builtin_fma(m1, B[4 * c + r], sel1[r]);
+      for (int pp = 0; pp < kPF; ++pp) {
+        const int p = 4 * c + pp;
+        const d2 ca = wa[pp];
+        const d2 cb = wb[pp];
+        const int so = base + ((pos + kPF) << 11);
+        wa[pp] = wload(wr, voff, so);
+        wb[pp] = wload(wr, voff, so + 1024);
+        ++pos;
+        acc0 = mfma64(ca.x, B[2 * p], acc0);
+        acc1 = mfma64(cb.x, B[2 * p], acc1);
+        acc0 = mfma64(ca.y, B[2 * p + 1], acc0);
+        acc1 = mfma64(cb.y, B[2 * p + 1], acc1);
+      }
+      if (SELECT && !tri) {
+        const double m = (c == ep) ? 1.0 : 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sel0[r] = __builtin_fma(m, B[8 * c + r], sel0[r]);
+          sel1[r] = __builtin_fma(m, B[8 * c + 4 + r], sel1[r]);
+        }
       }
     }
   }
 }
 
-template <int NS>
 __device__ __forceinline__ void prime_ring(__amdgpu_buffer_rsrc_t wr, int voff, int base,
                                            d2 (&wa)[kPF], d2 (&wb)[kPF]) {
 #pragma unroll
   for (int p = 0; p < kPF; ++p) {
-    if (p < NS / 2) {
-      wa[p] = wload(wr, voff, base + ((2 * p) << 10));
-      wb[p] = wload(wr, voff, base + ((2 * p + 1) << 10));
-    }
+    wa[p] = wload(wr, voff, base + (p << 11));
+    wb[p] = wload(wr, voff, base + (p << 11) + 1024);
   }
 }
 
@@ -184,6 +202,9 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
   const int voff = lane * 16;
+  // triangular variance formulation (set on the device by the K^-1 Cholesky, see
+  // predict_impl); uniform across the grid
+  const bool tri = !MULTI && !KMEM && a.tri_flag && __builtin_amdgcn_readfirstlane(*a.tri_flag) == 0;
 
   double top_v = -__builtin_inf();
   long long top_i = -1;
@@ -237,24 +258,41 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
         }
         const int base = o * w_obj + panel * w_panel;
         d2 wa[kPF], wb[kPF];
-        prime_ring<NS>(wr, voff, base, wa, wb);
+        prime_ring(wr, voff, base, wa, wb);
+        int pos = 0;
+        // multi-panel epilogue rows: K*[e][j], e = 32ep + 16h + g + 4r -> nxt[4h + r]
+        double nxt[8];
+        if (MULTI) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int e = 16 * (t >> 2) + g + 4 * (t & 3);
+            nxt[t] = KMEM ? kstar_at(a, o, e, j, valid) : pv * exp(sqdist<DIM>(xs, e, c) * nhl);
+          }
+        }
         for (int ep = 0; ep < n_ep; ++ep) {
           d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
           double sel0[4] = {0.0, 0.0, 0.0, 0.0}, sel1[4] = {0.0, 0.0, 0.0, 0.0};
-          panel_epair<NS, !MULTI>(wr, voff, base, ep, B, wa, wb, acc0, acc1, sel0, sel1);
           if (MULTI) {
-            // recompute K*[e][j] for the accumulator rows e = 16E + g + 4r
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int e0 = 32 * ep + g + 4 * r, e1 = e0 + 16;
-              if (KMEM) {
-                sel0[r] = kstar_at(a, o, e0, j, valid);
-                sel1[r] = kstar_at(a, o, e1, j, valid);
-              } else {
-                sel0[r] = pv * exp(sqdist<DIM>(xs, e0, c) * nhl);
-                sel1[r] = pv * exp(sqdist<DIM>(xs, e1, c) * nhl);
+            for (int r = 0; r < 4; ++r) { sel0[r] = nxt[r]; sel1[r] = nxt[4 + r]; }
+            if (KMEM) {
+#pragma unroll
+              for (int t = 0; t < 8; ++t) {
+                const int e = 32 * (ep + 1) + 16 * (t >> 2) + g + 4 * (t & 3);
+                nxt[t] = kstar_at(a, o, e, j, valid);
               }
             }
+          }
+          contract_epair<NS, DIM, !MULTI, MULTI && !KMEM>(wr, voff, base, pos, ep, tri, B, wa, wb,
+                                                          acc0, acc1, sel0, sel1, xs, c, pv, nhl,
+                                                          g, nxt);
+          if (tri) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              qpart = __builtin_fma(acc0[r], acc0[r], qpart);
+              qpart = __builtin_fma(acc1[r], acc1[r], qpart);
+            }
+            continue;
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -311,11 +349,17 @@ __global__ void pad_points_kernel(double* __restrict__ out, const double* __rest
   out[t] = r < rows ? (k < dim ? in[r * dim + k] : 0.0) : fill;
 }
 
-// Pack K^-1 (row-major, leading dim ld) into MFMA A-fragment order, zero padded:
-// out[o][panel][ep][pair][which][lane] (d2) = (W[16E + (l&15)][4s + (l>>4)], same at s+1),
-// E = 2ep + which, s = panel*NS + 2*pair (global k-step).
-__global__ void pack_kinv_kernel(d2* __restrict__ out, const double* __restrict__ kinv,
-                                 long long ld, int n, int n_pad, int ns_panel, int n_obj) {
+// Pack the A operand of the contraction into MFMA fragment order, zero padded.
+// Element (ep, pair, which, lane) of panel `panel` holds W[16E + (l&15)][4s + (l>>4)] and the
+// same at s+1 (E = 2ep + which, s = panel*ns_panel + 2*pair):
+//   dense:      W = K^-1 (row-major, leading dim ld); stream index = (panel, ep, pair)
+//   triangular: W = R^T with K^-1 = R R^T (R lower, dense n x n in `chol`), W[e][f] = R[f][e]
+//               for f >= e; only pairs >= 4ep are stored, stream index = off(ep) + pair - 4ep.
+// The choice is made on the device: triangular iff *tri_flag == 0 (Cholesky succeeded).
+__global__ void pack_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
+                            const double* __restrict__ chol, const int* __restrict__ tri_flag,
+                            int n, int n_pad, int ns_panel, int n_obj) {
+  const bool tri = tri_flag && *tri_flag == 0;
   const long long per_obj = (long long)n_pad * n_pad / 2;
   const long long total = per_obj * n_obj;
   const int n_ep = n_pad / 32;
@@ -332,12 +376,34 @@ __global__ void pack_kinv_kernel(d2* __restrict__ out, const double* __restrict_
     const int row = 16 * (2 * ep + which) + (lane & 15);
     const int s = panel * ns_panel + 2 * pair;
     const int col0 = 4 * s + (lane >> 4), col1 = col0 + 4;
-    const double* wo = kinv + (long long)o * ld * ld;
     d2 v;
-    v.x = (row < n && col0 < n) ? wo[(long long)row * ld + col0] : 0.0;
-    v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
-    out[t] = v;
+    long long dst = t;
+    if (tri) {
+      if (pair < 4 * ep) continue;
+      const long long off = (long long)ep * npair - 2LL * ep * (ep - 1);   // sum_{e<ep} (npair - 4e)
+      dst = (long long)o * per_obj + ((off + pair - 4 * ep) * 2 + which) * 64 + lane;
+      const double* ro = chol + (long long)o * n * n;
+      v.x = (row < n && col0 < n && col0 >= row) ? ro[(long long)col0 * n + row] : 0.0;
+      v.y = (row < n && col1 < n && col1 >= row) ? ro[(long long)col1 * n + row] : 0.0;
+    } else {
+      const double* wo = kinv + (long long)o * ld * ld;
+      v.x = (row < n && col0 < n) ? wo[(long long)row * ld + col0] : 0.0;
+      v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
+    }
+    out[dst] = v;
   }
+}
+
+// dense n x n copy of K^-1's leading block (the Cholesky input)
+__global__ void copy_square_kernel(double* __restrict__ dst, const double* __restrict__ src,
+                                   long long ld, int n, int n_obj) {
+  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long per = (long long)n * n;
+  if (t >= per * n_obj) return;
+  const int o = (int)(t / per);
+  const long long r = t - o * per;
+  const int i = (int)(r / n), j = (int)(r - (long long)i * n);
+  dst[t] = src[(long long)o * ld * ld + (long long)i * ld + j];
 }
 
 // alpha[o][f] = sum_e Kinv[o][f][e] * (y[e][o] - pm[o])   (numba_kernels.py:477-483),
@@ -409,7 +475,8 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct Plan {
   int n_pad, ns, n_panels, dim_pad, n_excl;
   bool multi;
-  size_t off_alpha, off_xpad, off_excl, off_partial, total;
+  size_t off_alpha, off_xpad, off_excl, off_partial, off_chol, off_status, total;
+  bool tri;
   int grid;
   size_t lds;
 };
@@ -426,11 +493,12 @@ int num_cus() {
   return cus;
 }
 
-int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device) {
+int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem = false) {
   if (!d || d->n_obj < 1 || d->n_obj > BO_MAX_OBJ || d->dim < 1 || d->dim > BO_MAX_DIM)
     return BO_ERR_ARG;
   if (d->n_train < 1 || d->n_cand < 0 || d->topq < 0 || d->topq > BO_MAX_TOPQ) return BO_ERR_ARG;
   if (d->cand_kind < 0 || d->cand_kind > 2) return BO_ERR_ARG;
+  if (d->mode != BO_PREDICT_AUTO && d->mode != BO_PREDICT_DENSE) return BO_ERR_ARG;
   if (d->excl_points && d->n_excl < 0) return BO_ERR_ARG;
   const long long n = d->n_train;
   if (n > (1 << 14)) return BO_ERR_UNSUPPORTED;
@@ -441,9 +509,9 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device) {
   else if (n_pad <= 64) ns = 16;
   else if (n_pad <= 128) ns = 32;
   else if (n_pad <= 256) ns = 64;
-  else if (n_pad <= 384) ns = 96;
-  else if (n_pad <= 512) ns = 128;
-  else { ns = kPanelSteps; multi = true; }
+  else if (n_pad <= 384 && !kmem) ns = 96;
+  else if (n_pad <= 512 && !kmem) ns = 128;
+  else { ns = kPanelSteps; multi = true; }   // (materialised-K* path: panels above 256 rows)
   n_pad = multi ? (int)((n + 511) / 512 * 512) : ns * 4;
   pl->n_pad = n_pad;
   pl->ns = ns;
@@ -464,8 +532,11 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device) {
   pl->off_excl = pl->off_xpad + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
   pl->off_partial = pl->off_excl + align256((size_t)(pl->n_excl + 1) * pl->dim_pad * sizeof(double));
   // partial lists sized for the largest persistent grid any device could use
-  pl->total = pl->off_partial +
-              align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry)) + 256;
+  pl->off_chol = pl->off_partial +
+                 align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry));
+  pl->tri = !multi && d->mode == BO_PREDICT_AUTO;
+  pl->off_status = pl->off_chol + (pl->tri ? align256((size_t)d->n_obj * n * n * sizeof(double)) : 0);
+  pl->total = pl->off_status + 256 + 256;
   return BO_OK;
 }
 
@@ -513,9 +584,7 @@ hipError_t launch_kmem(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
     case 8: return launch_fused<8, 2, false, true>(fa, pl.grid, pl.lds, s);
     case 16: return launch_fused<16, 2, false, true>(fa, pl.grid, pl.lds, s);
     case 32: return launch_fused<32, 2, false, true>(fa, pl.grid, pl.lds, s);
-    case 64: return launch_fused<64, 2, false, true>(fa, pl.grid, pl.lds, s);
-    case 96: return launch_fused<96, 2, false, true>(fa, pl.grid, pl.lds, s);
-    default: return launch_fused<128, 2, false, true>(fa, pl.grid, pl.lds, s);
+    default: return launch_fused<64, 2, false, true>(fa, pl.grid, pl.lds, s);
   }
 }
 
@@ -533,7 +602,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
                         void* workspace, size_t ws_bytes, void* stream) {
   const bool kmem = kstar != nullptr;
   Plan pl;
-  int st = make_plan(d, &pl, true);
+  int st = make_plan(d, &pl, true, kmem);
   if (st != BO_OK) return st;
   if (!workspace || ws_bytes < pl.total) return BO_ERR_WORKSPACE;
   if ((!kmem && !d->x_train) || !d->y_train || !d->kinv || d->ld_k < d->n_train ||
@@ -600,11 +669,26 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.kstar = kstar;
   fa.ks_rows = ks_rows;
 
+  const bool tri = pl.tri && !kmem;
+  double* chol = (double*)(ws + pl.off_chol);
+  int* tri_flag = (int*)(ws + pl.off_status);
+  fa.tri_flag = tri ? tri_flag : nullptr;
   {
+    if (tri) {
+      // K^-1 = R R^T on the device; a failed factorisation leaves *tri_flag = 1 and every
+      // later kernel of this call takes the dense formulation
+      BO_CHECK_HIP(hipMemsetAsync(tri_flag, 0, sizeof(int), s));
+      const long long nn = (long long)d->n_obj * d->n_train * d->n_train;
+      hipLaunchKernelGGL(copy_square_kernel, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s,
+                         chol, d->kinv, d->ld_k, (int)d->n_train, d->n_obj);
+      BO_CHECK_HIP(hipGetLastError());
+      const int pst = bo_internal_potrf(chol, (int)d->n_train, d->n_obj, tri_flag, s);
+      if (pst != BO_OK) return pst;
+    }
     const long long total = (long long)d->n_obj * pl.n_pad * pl.n_pad / 2;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(pack_kinv_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k,
-                       (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
+    hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, chol,
+                       fa.tri_flag, (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
     BO_CHECK_HIP(hipGetLastError());
     const long long rows = (long long)d->n_obj * pl.n_pad;
     hipLaunchKernelGGL(alpha_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, alpha,
@@ -662,13 +746,16 @@ static void fill_mv_desc(bo_predict_desc* d, int32_t n_obj, int64_t n_cand, int6
   d->n_cand = n_cand;
   d->grid_shape[0] = n_cand > 0 ? n_cand : 1;
   d->n_excl = 0;
+  d->mode = BO_PREDICT_DENSE;
 }
 
 size_t bo_update_mean_variance_workspace_size(int32_t n_obj, int64_t current_eval) {
   bo_predict_desc d;
   fill_mv_desc(&d, n_obj, 0, current_eval);
   d.excl_points = (const double*)1;  // no exclusion set
-  return bo_predict_workspace_size(&d);
+  Plan pl;
+  if (make_plan(&d, &pl, false, true) != BO_OK) return 0;
+  return pl.total;
 }
 
 int bo_update_mean_variance(double* mu, double* var, const double* k_star, int64_t ld_rows,

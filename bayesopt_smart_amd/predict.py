@@ -126,16 +126,22 @@ def _fill_desc(x_train, y_train, kinv, cands, pm, pv, ls, betas, offset, count, 
     return d
 
 
+MODES = {"auto": 0, "dense": 1}
+
+
 def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, prior_variance,
                     length_scales, betas, *, outputs=("mu", "var", "acq"), topq=0,
-                    excl_points=None, offset=0, count=None, out=None, device=None):
+                    excl_points=None, offset=0, count=None, out=None, device=None, mode="auto"):
     """Score candidates [offset, offset+count) of `cands`.
 
     x_train [N, d], y_train [N or T, n_obj] (only the first N rows are read), kinv
     [n_obj, N, N] (invert_k output) -- device f64 tensors or arrays.  Returns a dict with
     the requested outputs (device tensors [n_obj, count] / [count]) and, if topq > 0,
     ``top_val`` / ``top_idx`` (device [topq]; index -1 = no candidate).  Asynchronous
-    on the current stream.
+    on the current stream.  mode "auto" lets the library use the triangular variance
+    formulation q = |R^T k|^2 with K^-1 = R R^T (N <= 512, half the matrix-core work; falls
+    back to dense on the device if K^-1 is not numerically positive definite); "dense" is
+    update_variance's k^T (K^-1 k) verbatim.
     """
     dev = require_device(device)
     x_train = as_dev(x_train, dev)
@@ -155,6 +161,7 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
         raise ValueError(f"topq must be in [0, {_lib.MAX_TOPQ}]")
     desc = _fill_desc(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
                       betas, offset, count, excl_points, topq)
+    desc.mode = MODES[mode]
     res = {} if out is None else dict(out)
     for name in outputs:
         if name not in OUTPUT_NAMES:

@@ -52,6 +52,16 @@ def flops_per_candidate(n=N_TRAIN, n_obj=N_OBJ, d=DIM):
     return n_obj * (2 * n * n + 6 * n) + (3 * d - 1) * n
 
 
+def executed_mfma_flops_per_candidate(mode, n=N_TRAIN, n_obj=N_OBJ):
+    """Matrix-core flops the fused kernel actually issues per candidate (16x16x4 f64 MFMA,
+    2048 flops, 16 candidates per wave): dense walks all (NS/8) E-pairs x (NS/2) k-step pairs,
+    triangular only the upper chunks c >= ep."""
+    ns = -(-n // 4)
+    ns = next(v for v in (8, 16, 32, 64, 96, 128) if v >= ns) if n <= 512 else ns
+    pairs = ns * ns // 16 if mode == "dense" else ns * ns // 32 + ns // 4
+    return n_obj * pairs * 4 * 2048 // 16
+
+
 def toy_function(x):
     """examples/benchmark_functions.py:33-50."""
     return np.stack([-((x[:, 0] - 150) ** 2) + 100, -((x[:, 1] - 150) ** 2) + 20], axis=1)
@@ -121,6 +131,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("auto", "dense"), default="auto",
+                    help="variance formulation (auto = triangular |R^T k|^2 when N <= 512)")
     args = ap.parse_args()
 
     import torch
@@ -154,7 +166,8 @@ def main():
 
     def step():
         r = bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=("mu", "var", "acq"),
-                               topq=TOPQ, offset=offset, count=per_rank, out=out, device=dev)
+                               topq=TOPQ, offset=offset, count=per_rank, out=out, device=dev,
+                               mode=args.mode)
         if world > 1:
             dist.all_gather_into_tensor(gath_v, r["top_val"])
             dist.all_gather_into_tensor(gath_i, r["top_idx"])
@@ -189,6 +202,7 @@ def main():
 
     if rank == 0:
         f = flops_per_candidate()
+        fx = executed_mfma_flops_per_candidate(args.mode)
         achieved = f * per_rank / (k_ms * 1e-3) / 1e12
         res = {
             "metric": "candidate-points/sec (GP predict + HVI) at N_train=512, N_cand=1M",
@@ -211,7 +225,12 @@ def main():
                          "unit": "TFLOP/s", "frac": achieved / PEAK_F64_MATRIX_TFLOPS,
                          "traffic": pmc_traffic(),
                          "kernel": "fused_predict_kernel<128,2,false,false>",
-                         "kernel_ms": k_ms, "flops_per_candidate": f},
+                         "kernel_ms": k_ms, "flops_per_candidate": f,
+                         "formulation": ("triangular: K^-1 = R R^T, q = |R^T k|^2" if args.mode == "auto"
+                                         else "dense: q = k^T (K^-1 k)"),
+                         "executed_mfma_flops_per_candidate": fx,
+                         "executed_mfma_tflops": fx * per_rank / (k_ms * 1e-3) / 1e12,
+                         "executed_mfma_frac": fx * per_rank / (k_ms * 1e-3) / 1e12 / PEAK_F64_MATRIX_TFLOPS},
             "selected": [int(i) for i in sel[1]],
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -63,6 +63,13 @@ int bo_device_count(void);
  * No N x M k_star array is materialised: candidate tiles are generated, contracted
  * against K^-1 on the f64 matrix cores and reduced to outputs in one pass.
  * ---------------------------------------------------------------------------------- */
+/* Variance formulation.  DENSE: q = k^T (K^-1 k) exactly as update_variance (2N^2 flops per
+ * candidate and objective).  AUTO: when N <= 512 the library factors the given K^-1 = R R^T
+ * (Cholesky, on the device) and computes q = |R^T k|^2 (N^2 flops: half the matrix-core
+ * work); if that factorisation fails (K^-1 not numerically positive definite) it falls back
+ * to DENSE on the device, without a host round trip. */
+typedef enum bo_predict_mode { BO_PREDICT_AUTO = 0, BO_PREDICT_DENSE = 1 } bo_predict_mode;
+
 typedef struct bo_predict_desc {
   int32_t n_obj;              /* objectives (<= BO_MAX_OBJ)                                 */
   int32_t dim;                /* input dimensions (<= BO_MAX_DIM)                            */
@@ -73,7 +80,7 @@ typedef struct bo_predict_desc {
   const double* kinv;         /* device [n_obj][ld_k][ld_k]; leading N x N block = invert_k() */
   int64_t ld_k;
   int32_t cand_kind;          /* bo_cand_kind                                                 */
-  int32_t reserved0;
+  int32_t mode;               /* bo_predict_mode                                              */
   const void* cand;           /* device [n_cand][dim] (kinds I64/F64)                         */
   int64_t n_cand;             /* candidates scored by this call                               */
   int64_t cand_offset;        /* global index of this call's first candidate                  */

@@ -23,10 +23,10 @@ def bo():
     return bo
 
 
-def _run(bo, d, cands, q=16, outputs=ALL, excl=None):
+def _run(bo, d, cands, q=16, outputs=ALL, excl=None, mode="auto"):
     import torch
     res = bo.predict.predict_acquire(d["x"], d["y"], d["Kinv"], cands, d["pm"], d["pv"], d["ls"],
-                                     d["betas"], outputs=outputs, topq=q, excl_points=excl)
+                                     d["betas"], outputs=outputs, topq=q, excl_points=excl, mode=mode)
     torch.cuda.synchronize()
     out = {k: v.cpu().numpy() for k, v in res.items() if not k.startswith("_")}
     return out
@@ -49,11 +49,12 @@ def test_mfma_f64_layout(bo):
     np.testing.assert_array_equal(td.cpu().numpy(), a @ b)
 
 
+@pytest.mark.parametrize("mode", ["auto", "dense"])
 @pytest.mark.parametrize("name", ["g1_predict_2d", "g2_predict_512", "g3_predict_6d3o"])
-def test_predict_vs_reference_golden(bo, name):
+def test_predict_vs_reference_golden(bo, name, mode):
     d = predict_fixture(name)
     cands = bo.predict.CandidateSet.explicit(d["cand"])
-    out = _run(bo, d, cands)
+    out = _run(bo, d, cands, mode=mode)
     check_predict(out, d, d["pv"])
     excl = _excluded(d["cand"], d["x"])
     check_topq(out["top_idx"], d["acq"], excl, 16)
@@ -75,8 +76,10 @@ def test_predict_implicit_grid(bo):
     np.testing.assert_array_equal(cands.points(out["top_idx"][:3]), d["select_q3"])
 
 
-@pytest.mark.parametrize("n,dim,n_obj", [(7, 2, 2), (33, 3, 1), (130, 5, 4), (600, 2, 2), (1100, 6, 3)])
-def test_predict_shapes_vs_oracle(bo, n, dim, n_obj):
+@pytest.mark.parametrize("mode", ["auto", "dense"])
+@pytest.mark.parametrize("n,dim,n_obj", [(7, 2, 2), (33, 3, 1), (130, 5, 4), (300, 2, 3), (600, 2, 2),
+                                         (1100, 6, 3)])
+def test_predict_shapes_vs_oracle(bo, n, dim, n_obj, mode):
     rng = np.random.default_rng(n)
     m = 3000
     side = 400 if dim == 2 else 60
@@ -98,7 +101,7 @@ def test_predict_shapes_vs_oracle(bo, n, dim, n_obj):
     kinv = O.invert_k(n, km)
     ref = O.predict_acquire(x, y, cand, pm, pv, ls, betas, kinv=kinv)
     d = dict(x=x, y=y, Kinv=kinv, pm=pm, pv=pv, ls=ls, betas=betas)
-    out = _run(bo, d, bo.predict.CandidateSet.explicit(cand), q=8)
+    out = _run(bo, d, bo.predict.CandidateSet.explicit(cand), q=8, mode=mode)
     check_predict(out, ref, pv)
     check_topq(out["top_idx"], ref["acq"], _excluded(cand, x), 8)
 
@@ -167,6 +170,8 @@ def test_full_size_c3_properties(bo):
     out2 = _run(bo, d, cands, q=16, outputs=("acq",))
     np.testing.assert_array_equal(out["acq"], out2["acq"])
     np.testing.assert_array_equal(out["top_idx"], out2["top_idx"])
+    dense = _run(bo, d, cands, q=16, outputs=("mu", "var", "acq"), mode="dense")
+    check_predict({k: dense[k] for k in ("mu", "var", "acq")}, {k: out[k] for k in ("mu", "var", "acq")}, pv)
     sub = np.sort(rng.choice(side * side, size=4096, replace=False))
     pts = cands.points(sub)
     ref = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv)
