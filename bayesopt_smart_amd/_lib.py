@@ -22,7 +22,7 @@ MAX_TOPQ = 48
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_WORKSPACE, ERR_HIP, ERR_NOT_PD, ERR_SINGULAR = range(7)
 CAND_I64, CAND_F64, CAND_GRID = 0, 1, 2
-MODE_AUTO, MODE_DENSE = 0, 1
+MODE_AUTO, MODE_DENSE, MODE_NO_SEPARABLE = 0, 1, 2
 
 c_dbl_p = C.POINTER(C.c_double)
 c_vp = C.c_void_p

@@ -143,18 +143,25 @@ __global__ void corr_kernel(double* __restrict__ dst, const double* __restrict__
 
 // Factor diagonal block kb (every block does it in LDS) and solve its own row block
 // ib = kb + blockIdx.x: L_ib = A_ib L_kk^-T.  Lower triangle only; in place.
+// The panel solve goes through W = L_kk^-1 (one column per lane, register-resident forward
+// substitution) so the 32 x 32 product X = A_ib W^T runs fully parallel.
 __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ C, int n, int kb,
                                                          int* __restrict__ status) {
   __shared__ double Lk[NB][NB + 1];
+  __shared__ double Wi[NB][NB + 1];
   __shared__ double Ab[NB][NB + 1];
   const int o = blockIdx.y;
   double* c = C + (long long)o * n * n;
   const int k0 = kb * NB;
   const int kn = min(NB, n - k0);
+  const int ib = kb + blockIdx.x;
+  const int i0 = ib * NB;
+  const int in = min(NB, n - i0);
   const int tid = threadIdx.x;
   for (int t = tid; t < NB * NB; t += 256) {
     const int r = t / NB, q = t % NB;
-    Lk[r][q] = (r < kn && q < kn && q <= r) ? c[(long long)(k0 + r) * n + k0 + q] : 0.0;
+    Lk[r][q] = (r < kn && q < kn && q <= r) ? c[(long long)(k0 + r) * n + k0 + q] : (r == q ? 1.0 : 0.0);
+    if (ib != kb) Ab[r][q] = (r < in && q < kn) ? c[(long long)(i0 + r) * n + k0 + q] : 0.0;
   }
   __syncthreads();
   // unblocked right-looking Cholesky of the diagonal block (LAPACK potf2 order of terms)
@@ -162,10 +169,10 @@ __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ C,
   for (int j = 0; j < kn; ++j) {
     const double d = Lk[j][j];
     if (!(d > 0.0)) bad = true;
-    const double s = sqrt(d);
+    const double sd = sqrt(d);
     __syncthreads();
-    if (tid == 0) Lk[j][j] = s;
-    for (int r = j + 1 + tid; r < kn; r += 256) Lk[r][j] = Lk[r][j] / s;
+    if (tid == 0) Lk[j][j] = sd;
+    for (int r = j + 1 + tid; r < kn; r += 256) Lk[r][j] = Lk[r][j] / sd;
     __syncthreads();
     for (int t = tid; t < kn * kn; t += 256) {
       const int r = t / kn, q = t % kn;
@@ -173,7 +180,6 @@ __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ C,
     }
     __syncthreads();
   }
-  const int ib = kb + blockIdx.x;
   if (ib == kb) {
     if (bad && tid == 0) atomicOr(status, 1);
     for (int t = tid; t < kn * kn; t += 256) {
@@ -182,25 +188,34 @@ __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ C,
     }
     return;
   }
-  const int i0 = ib * NB;
-  const int in = min(NB, n - i0);
-  for (int t = tid; t < NB * NB; t += 256) {
-    const int r = t / NB, q = t % NB;
-    Ab[r][q] = (r < in && q < kn) ? c[(long long)(i0 + r) * n + k0 + q] : 0.0;
-  }
-  __syncthreads();
-  if (tid < in) {
-    const int r = tid;
-    for (int j = 0; j < kn; ++j) {
-      double x = Ab[r][j];
-      for (int t = 0; t < j; ++t) x = __builtin_fma(-Ab[r][t], Lk[j][t], x);
-      Ab[r][j] = x / Lk[j][j];
+  // W = L_kk^-1: lane `col` forward-substitutes the unit vector e_col (rows >= kn are
+  // identity-padded, so W stays well defined for a partial last block)
+  if (tid < NB) {
+    const int col = tid;
+    double x[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      double v = (j == col) ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = 0; t < j; ++t) v = __builtin_fma(-Lk[j][t], x[t], v);
+      x[j] = (j < col) ? 0.0 : v / Lk[j][j];
     }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) Wi[j][col] = x[j];
   }
   __syncthreads();
-  for (int t = tid; t < in * kn; t += 256) {
-    const int r = t / kn, q = t % kn;
-    c[(long long)(i0 + r) * n + k0 + q] = Ab[r][q];
+  // X[r][j] = sum_{t <= j} A[r][t] W[j][t]
+  {
+    const int r = tid >> 3, jg = (tid & 7) * 4;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < NB; ++t) {
+      const double av = Ab[r][t];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = __builtin_fma(av, Wi[jg + u][t], acc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (r < in && jg + u < kn) c[(long long)(i0 + r) * n + k0 + jg + u] = acc[u];
   }
 }
 

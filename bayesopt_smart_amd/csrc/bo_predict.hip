@@ -30,12 +30,29 @@
 
 #include <vector>
 
+#ifdef BO_ABL_STAMPS
+// Diagnostic build only: per-wave phase cycle sums (s_memtime), never in a product build.
+__device__ unsigned long long g_stamps[4096][8];
+#define STAMP(var)                                                                    \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");      \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  } while (0)
+#else
+#define STAMP(var) do { } while (0)
+#endif
+
 namespace {
 
 constexpr int kWaves = 4;               // waves per workgroup
 constexpr int kTile = 16 * kWaves;      // candidates per workgroup tile
 constexpr int kPanelSteps = 128;        // k-steps of 4 training rows per register panel (512 rows)
+#ifdef BO_ABL_PF8
+constexpr int kPF = 8;                  // ablation: 8 pairs in flight (dense mode only)
+#else
 constexpr int kPF = 4;                  // prefetch depth (pairs of k-steps)
+#endif
 
 struct FusedArgs {
   int n_obj, dim, n_train, n_pad;       // n_pad = padded training rows (multiple of 32)
@@ -56,6 +73,12 @@ struct FusedArgs {
   const double* kstar;                   // KMEM: materialised k_star [n_obj][ks_rows][n_cand]
   long long ks_rows;
   const int* tri_flag;                   // device: 0 => K^-1 = R R^T factored, use R^T (triangular)
+  // separable K* on an integer grid (see sep_generate): device flag (0 => usable), last-axis
+  // extent S and lower bound, LDS offsets (doubles) of the exp tables and per-wave R scratch
+  const int* sep_flag;
+  int sep_S;
+  long long sep_lo;
+  int off_tbl, off_rw;
 };
 
 template <int DIM>
@@ -133,12 +156,16 @@ template <int NS, int DIM, bool SELECT, bool RECOMP>
 __device__ __forceinline__ void contract_epair(__amdgpu_buffer_rsrc_t wr, int voff, int base,
                                                int& pos, int ep, bool tri, const double (&B)[NS],
                                                d2 (&wa)[kPF], d2 (&wb)[kPF], d4& acc0, d4& acc1,
+                                               d4& acc2, d4& acc3,
                                                double (&sel0)[4], double (&sel1)[4],
                                                const double* xs, const double (&cc)[DIM],
                                                double pv, double nhl, int g, double (&nxt)[8]) {
   constexpr int NCH = NS / 8;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
+#ifdef BO_ABL_SYNCCHUNK
+    if (!tri || c >= ep) __builtin_amdgcn_s_barrier();
+#endif
     if (RECOMP && c < 8) {
       // row of E-pair ep+1 for slot c: e = 32(ep+1) + 16(c>>2) + g + 4(c&3)
       const int e = 32 * (ep + 1) + 16 * (c >> 2) + g + 4 * (c & 3);
@@ -146,18 +173,29 @@ __device__ __forceinline__ void contract_epair(__amdgpu_buffer_rsrc_t wr, int vo
     }
     if (!tri || c >= ep) {
 #pragma unroll
-      for (int pp = 0; pp < kPF; ++pp) {
+      for (int pp = 0; pp < 4; ++pp) {
         const int p = 4 * c + pp;
-        const d2 ca = wa[pp];
-        const d2 cb = wb[pp];
+        const int sl = (kPF == 8) ? 4 * (c & 1) + pp : pp;   // PF8: valid for dense streams only
+        const d2 ca = wa[sl];
+        const d2 cb = wb[sl];
         const int so = base + ((pos + kPF) << 11);
-        wa[pp] = wload(wr, voff, so);
-        wb[pp] = wload(wr, voff, so + 1024);
+#ifndef BO_ABL_NOLOAD
+        wa[sl] = wload(wr, voff, so);
+        wb[sl] = wload(wr, voff, so + 1024);
+#else   // ablation build only: keep the stream's address arithmetic, drop the loads
+        wa[pp] = ca * 0.999 + (double)so;
+        wb[pp] = cb * 0.999;
+#endif
         ++pos;
         acc0 = mfma64(ca.x, B[2 * p], acc0);
         acc1 = mfma64(cb.x, B[2 * p], acc1);
+#ifdef BO_ABL_ACC4
+        acc2 = mfma64(ca.y, B[2 * p + 1], acc2);
+        acc3 = mfma64(cb.y, B[2 * p + 1], acc3);
+#else
         acc0 = mfma64(ca.y, B[2 * p + 1], acc0);
         acc1 = mfma64(cb.y, B[2 * p + 1], acc1);
+#endif
       }
       if (SELECT && !tri) {
         const double m = (c == ep) ? 1.0 : 0.0;
@@ -195,8 +233,21 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
   for (int t = tid; t < a.n_pad * DIM; t += blockDim.x) xs[t] = a.xpad[t];
   for (int t = tid; t < a.n_obj * a.n_pad; t += blockDim.x) alpha[t] = a.alpha[t];
   const double* exs = a.excl ? exs_buf : xs;   // NULL: the evaluated points are x_train
+  const int n_excl = a.excl ? a.n_excl : a.n_train;
   if (a.excl)
     for (int t = tid; t < a.n_excl * DIM; t += blockDim.x) exs_buf[t] = a.excl[t];
+  // separable K* (integer grid, single panel): T_o[m + S - 1] = exp(nhl_o m^2)
+  const bool sep = !MULTI && !KMEM && a.sep_flag &&
+                   __builtin_amdgcn_readfirstlane(*a.sep_flag) == 0;
+  double* tbl = smem + a.off_tbl;
+  double* rw = smem + a.off_rw + wave * a.n_pad * 2;     // [n_pad] x (R, x_last)
+  const int TS = 2 * a.sep_S - 1;
+  if (sep)
+    for (int t = tid; t < a.n_obj * TS; t += blockDim.x) {
+      const int o = t / TS;
+      const double m = (double)(t - o * TS - (a.sep_S - 1));
+      tbl[t] = exp(a.nhl[o] * (m * m));
+    }
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t wr =
@@ -212,7 +263,16 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
   const int w_obj = a.n_pad * a.n_pad * 8;                 // bytes per objective
   const int w_panel = a.n_pad * (NS * 4) * 8;              // bytes per panel
 
+#ifdef BO_ABL_STAMPS
+  unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_a = 0, t_b = 0;
+#endif
   for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+#ifdef BO_ABL_STAMPS
+    STAMP(t_b);
+    if (tile != blockIdx.x) st_sum[4] += t_b - t_a;   // top-q insert + loop overhead
+    t_a = t_b;
+#endif
     const long long j = tile * kTile + wave * 16 + jl;
     const bool valid = j < a.n_cand;
     double c[DIM];
@@ -224,8 +284,12 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
 
     // exclusion (acquisition.py:137-139): candidate equal, coordinate by coordinate, to an
     // evaluated point.  Lane group g checks points g, g+4, ...
+    // With the default set (the training points, a.excl == nullptr) the test is folded into
+    // objective 0's K* generation below: all coordinates equal <=> squared distance == 0
+    // (finite coordinates).
     bool hit = false;
-    for (int e = g; e < (KMEM ? 0 : a.n_excl); e += 4) {
+    // (multi-panel kernels keep the explicit loop: their register budget is tighter)
+    for (int e = g; e < ((KMEM || (!MULTI && !a.excl)) ? 0 : n_excl); e += 4) {
       const d2* r = (const d2*)(exs + e * DIM);
       bool eq = true;
 #pragma unroll
@@ -235,11 +299,10 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
       }
       hit = hit || eq;
     }
-    const unsigned long long hb = __ballot(hit);
-    const bool excluded =
-        ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
-
     double acq = 0.0;
+#ifdef BO_ABL_STAMPS
+    STAMP(t_b); st_sum[0] += t_b - t_a; t_a = t_b;   // candidate load + exclusion
+#endif
     for (int o = 0; o < a.n_obj; ++o) {
       const double pv = a.pv[o], nhl = a.nhl[o];
       const double* al = alpha + o * a.n_pad;
@@ -249,15 +312,66 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
         // K* block for this lane: B[s] = K*[f0 + 4s + g][j]  (numba_kernels.py:440-442);
         // padded rows sit at 1e200 so their exp underflows to exactly 0.
         double B[NS];
+        if (sep) {
+          // K*[f][j] = pv exp(nhl |x_f - c_j|^2) = pv * R(f) * T[x_f,last - c_j,last]: the 16
+          // candidates of a wave share every coordinate but the last (one grid row), so the
+          // first factor R(f) = exp(nhl sum_{k != last} (x_fk - c_k)^2) is computed once per
+          // row f by the wave (8 exps per lane at N = 512) and the second is a table lookup.
+          // R is stored negated when that partial distance is 0 (exclusion test below).
+          __syncthreads();                       // rw of the previous objective fully consumed
+          for (int f = lane; f < a.n_pad; f += 64) {
+            const double* r = xs + f * DIM;
+            double sqs = 0.0;
+#pragma unroll
+            for (int k = 0; k < DIM; ++k)
+              if (k != a.dim - 1) { const double d = r[k] - c[k]; sqs = __builtin_fma(d, d, sqs); }
+            double rv = f < a.n_train ? exp(sqs * nhl) : 0.0;
+            if (f < a.n_train && sqs == 0.0) rv = -rv;
+            d2 e;
+            e.x = rv;
+            e.y = f < a.n_train ? r[a.dim - 1] : 0.0;   // last coordinate (integral)
+            ((d2*)rw)[f] = e;
+          }
+          __syncthreads();
+          double cl = 0.0;
+#pragma unroll
+          for (int k = 0; k < DIM; ++k)
+            if (k == a.dim - 1) cl = c[k];
+          const int ci = (int)cl - (a.sep_S - 1);   // index = x_last - c_last + S - 1
+          const double* to = tbl + o * TS;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const int f = 4 * s + g;
+            const d2 e = ((const d2*)rw)[f];
+            const int xi = (int)e.y;
+            const int idx = min(max(xi - ci, 0), TS - 1);
+            const double tv = to[idx];
+            B[s] = pv * (fabs(e.x) * tv);
+            if (!a.excl && o == 0) hit = hit || (e.x < 0.0 && xi == (int)cl);
+            if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+          }
+        } else
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const int f = f0 + 4 * s + g;
-          if (KMEM) B[s] = kstar_at(a, o, f, j, valid);
-          else B[s] = pv * exp(sqdist<DIM>(xs, f, c) * nhl);
+          if (KMEM) {
+            B[s] = kstar_at(a, o, f, j, valid);
+          } else {
+            const double sq = sqdist<DIM>(xs, f, c);
+            if (!MULTI && !a.excl && o == 0) hit = hit || (sq == 0.0);
+#ifndef BO_ABL_NOEXP
+            B[s] = pv * exp(sq * nhl);
+#else   // ablation build only: K* without the exp
+            B[s] = pv * (sq * nhl);
+#endif
+          }
           if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         const int base = o * w_obj + panel * w_panel;
         d2 wa[kPF], wb[kPF];
+#ifdef BO_ABL_STAMPS
+        STAMP(t_b); st_sum[1] += t_b - t_a; t_a = t_b;   // K* generation (exp)
+#endif
         prime_ring(wr, voff, base, wa, wb);
         int pos = 0;
         // multi-panel epilogue rows: K*[e][j], e = 32ep + 16h + g + 4r -> nxt[4h + r]
@@ -270,7 +384,11 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
           }
         }
         for (int ep = 0; ep < n_ep; ++ep) {
+#ifdef BO_ABL_SYNCEP
+          __builtin_amdgcn_s_barrier();
+#endif
           d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+          d4 acc2 = {0.0, 0.0, 0.0, 0.0}, acc3 = {0.0, 0.0, 0.0, 0.0};
           double sel0[4] = {0.0, 0.0, 0.0, 0.0}, sel1[4] = {0.0, 0.0, 0.0, 0.0};
           if (MULTI) {
 #pragma unroll
@@ -284,8 +402,12 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
             }
           }
           contract_epair<NS, DIM, !MULTI, MULTI && !KMEM>(wr, voff, base, pos, ep, tri, B, wa, wb,
-                                                          acc0, acc1, sel0, sel1, xs, c, pv, nhl,
+                                                          acc0, acc1, acc2, acc3, sel0, sel1, xs, c, pv, nhl,
                                                           g, nxt);
+#ifdef BO_ABL_ACC4
+          acc0 += acc2;
+          acc1 += acc3;
+#endif
           if (tri) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -304,6 +426,9 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
         for (int s = 0; s < NS; ++s) mpart = __builtin_fma(al[f0 + 4 * s + g], B[s], mpart);
       }
       // reduce over the 4 lane groups holding the same candidate
+#ifdef BO_ABL_STAMPS
+      STAMP(t_b); st_sum[2] += t_b - t_a; t_a = t_b;   // contraction (MFMA loop + mu dot)
+#endif
       qpart += __shfl_xor(qpart, 16, 64);
       qpart += __shfl_xor(qpart, 32, 64);
       mpart += __shfl_xor(mpart, 16, 64);
@@ -325,17 +450,41 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
         if (a.ucb) a.ucb[off] = u;
       }
     }
+#ifdef BO_ABL_STAMPS
+    STAMP(t_b); st_sum[3] += t_b - t_a; t_a = t_b;   // per-objective epilogues + stores
+#endif
     if (valid && g == 0 && a.acq) a.acq[j] = acq;
     if (a.topq > 0) {
+      const unsigned long long hb = __ballot(hit);
+      const bool excluded =
+          ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
       const long long gi = (valid && !excluded) ? a.cand_offset + j : -1;
       bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
     }
   }
+#ifdef BO_ABL_STAMPS
+  if (lane == 0) {
+    const int w = blockIdx.x * kWaves + wave;
+    for (int k = 0; k < 5; ++k) g_stamps[w][k] = st_sum[k];
+    g_stamps[w][4] = 1;
+  }
+#endif
   if (a.topq > 0 && lane < a.topq) {
     TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
     dst[lane].v = top_v;
     dst[lane].i = top_i;
   }
+}
+
+// Separable-K* precondition on the training rows: last coordinate integral and inside the
+// grid's last axis [lo, lo + S - 1] (else *flag = 1 and the kernel keeps the exp path).
+__global__ void sep_check_kernel(const double* __restrict__ x, int n, int dim, long long lo, int S,
+                                 int* __restrict__ flag) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  const double v = x[(long long)f * dim + dim - 1];
+  const bool ok = v == __builtin_rint(v) && v >= (double)lo && v <= (double)(lo + S - 1);
+  if (!ok) atomicOr(flag, 1);
 }
 
 // Training rows / evaluated points padded to [rows_pad][DIM]: coordinates beyond `dim`
@@ -477,6 +626,8 @@ struct Plan {
   bool multi;
   size_t off_alpha, off_xpad, off_excl, off_partial, off_chol, off_status, total;
   bool tri;
+  bool sep;
+  int off_tbl, off_rw;   // LDS offsets in doubles
   int grid;
   size_t lds;
 };
@@ -498,7 +649,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
     return BO_ERR_ARG;
   if (d->n_train < 1 || d->n_cand < 0 || d->topq < 0 || d->topq > BO_MAX_TOPQ) return BO_ERR_ARG;
   if (d->cand_kind < 0 || d->cand_kind > 2) return BO_ERR_ARG;
-  if (d->mode != BO_PREDICT_AUTO && d->mode != BO_PREDICT_DENSE) return BO_ERR_ARG;
+  if (d->mode & ~(BO_PREDICT_DENSE | BO_PREDICT_NO_SEPARABLE)) return BO_ERR_ARG;
   if (d->excl_points && d->n_excl < 0) return BO_ERR_ARG;
   const long long n = d->n_train;
   if (n > (1 << 14)) return BO_ERR_UNSUPPORTED;
@@ -519,9 +670,24 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   pl->n_panels = multi ? n_pad / 512 : 1;
   pl->dim_pad = pad_dim(d->dim);
   pl->n_excl = (int)(d->excl_points ? d->n_excl : n);
-  pl->lds = ((size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad +
-             (d->excl_points ? (size_t)pl->n_excl * pl->dim_pad : 0)) * sizeof(double);
+  const size_t lds_base = (size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad +
+                         (d->excl_points ? (size_t)pl->n_excl * pl->dim_pad : 0);
+  pl->lds = lds_base * sizeof(double);
   if (pl->lds > 160 * 1024) return BO_ERR_UNSUPPORTED;
+  // separable K* for the integer grid (one row per 16-candidate wave tile)
+  pl->sep = false;
+  pl->off_tbl = pl->off_rw = 0;
+  if (!multi && !kmem && d->cand_kind == BO_CAND_GRID && !(d->mode & BO_PREDICT_NO_SEPARABLE)) {
+    const long long S = d->grid_shape[d->dim - 1];
+    const size_t extra = (size_t)d->n_obj * (2 * S - 1) + (size_t)kWaves * n_pad * 2;
+    if (S % 16 == 0 && S <= 32768 && d->cand_offset % 16 == 0 &&
+        (lds_base + extra) * sizeof(double) <= 160 * 1024) {
+      pl->sep = true;
+      pl->off_tbl = (int)lds_base;
+      pl->off_rw = (int)(lds_base + (size_t)d->n_obj * (2 * S - 1));
+      pl->lds = (lds_base + extra) * sizeof(double);
+    }
+  }
   const size_t w_bytes = (size_t)d->n_obj * n_pad * n_pad * sizeof(double);
   if (w_bytes >= (1ull << 31)) return BO_ERR_UNSUPPORTED;
   const long long n_tiles = (d->n_cand + kTile - 1) / kTile;
@@ -534,9 +700,9 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   // partial lists sized for the largest persistent grid any device could use
   pl->off_chol = pl->off_partial +
                  align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry));
-  pl->tri = !multi && d->mode == BO_PREDICT_AUTO;
+  pl->tri = !multi && !(d->mode & BO_PREDICT_DENSE);
   pl->off_status = pl->off_chol + (pl->tri ? align256((size_t)d->n_obj * n * n * sizeof(double)) : 0);
-  pl->total = pl->off_status + 256 + 256;
+  pl->total = pl->off_status + 256 + 256;   // +0: tri status, +16: separable-K* status
   return BO_OK;
 }
 
@@ -673,6 +839,18 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   double* chol = (double*)(ws + pl.off_chol);
   int* tri_flag = (int*)(ws + pl.off_status);
   fa.tri_flag = tri ? tri_flag : nullptr;
+  int* sep_flag = (int*)(ws + pl.off_status + 16);
+  fa.sep_flag = pl.sep ? sep_flag : nullptr;
+  fa.sep_S = pl.sep ? (int)d->grid_shape[d->dim - 1] : 1;
+  fa.sep_lo = pl.sep ? d->grid_lo[d->dim - 1] : 0;
+  fa.off_tbl = pl.off_tbl;
+  fa.off_rw = pl.off_rw;
+  if (pl.sep) {
+    BO_CHECK_HIP(hipMemsetAsync(sep_flag, 0, sizeof(int), s));
+    hipLaunchKernelGGL(sep_check_kernel, dim3((unsigned)((d->n_train + 255) / 256)), dim3(256), 0, s,
+                       d->x_train, (int)d->n_train, d->dim, (long long)fa.sep_lo, fa.sep_S, sep_flag);
+    BO_CHECK_HIP(hipGetLastError());
+  }
   {
     if (tri) {
       // K^-1 = R R^T on the device; a failed factorisation leaves *tri_flag = 1 and every
@@ -809,6 +987,14 @@ int bo_profile_stop(double* total_ms, int* launches) {
   g_timer.used = 0;
   return BO_OK;
 }
+
+#ifdef BO_ABL_STAMPS
+int bo_debug_stamps(unsigned long long* host, int n_waves) {
+  BO_CHECK_HIP(hipDeviceSynchronize());
+  BO_CHECK_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * n_waves));
+  return BO_OK;
+}
+#endif
 
 int bo_selftest_mfma_f64(const double* a, const double* b, double* dd, void* stream) {
   if (!a || !b || !dd) return BO_ERR_ARG;

@@ -15,13 +15,15 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
-LIB = os.path.join(PKG, "libbo_amd.so")
-BUILD = os.path.join(HERE, "build")
+VARIANT = os.environ.get("BO_BUILD_VARIANT", "")      # ablation builds: e.g. "NOEXP"
+LIB = os.path.join(PKG, f"libbo_amd{('_' + VARIANT.lower().replace(',', '_')) if VARIANT else ''}.so")
+BUILD = os.path.join(HERE, "build" + (("_" + VARIANT.lower()) if VARIANT else ""))
 SOURCES = ["bo_predict.hip", "bo_fit.hip", "bo_select.hip", "bo_misc.hip"]
 HEADERS = ["bo_common.h", os.path.join("..", "..", "include", "bo_amd.h")]
 ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         "-I", os.path.join(ROOT, "include")]
+         "-I", os.path.join(ROOT, "include")] + \
+        [f"-DBO_ABL_{v}" for v in VARIANT.split(",") if v]
 
 
 def _hipcc():

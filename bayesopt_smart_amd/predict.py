@@ -126,7 +126,7 @@ def _fill_desc(x_train, y_train, kinv, cands, pm, pv, ls, betas, offset, count, 
     return d
 
 
-MODES = {"auto": 0, "dense": 1}
+MODES = {"auto": 0, "dense": 1, "auto-exp": 2, "dense-exp": 3}
 
 
 def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, prior_variance,
@@ -141,7 +141,8 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     on the current stream.  mode "auto" lets the library use the triangular variance
     formulation q = |R^T k|^2 with K^-1 = R R^T (N <= 512, half the matrix-core work; falls
     back to dense on the device if K^-1 is not numerically positive definite); "dense" is
-    update_variance's k^T (K^-1 k) verbatim.
+    update_variance's k^T (K^-1 k) verbatim.  The "-exp" modes disable the integer-grid
+    separable K* generation (exp table) and evaluate every K* entry with exp().
     """
     dev = require_device(device)
     x_train = as_dev(x_train, dev)

@@ -68,7 +68,16 @@ int bo_device_count(void);
  * (Cholesky, on the device) and computes q = |R^T k|^2 (N^2 flops: half the matrix-core
  * work); if that factorisation fails (K^-1 not numerically positive definite) it falls back
  * to DENSE on the device, without a host round trip. */
-typedef enum bo_predict_mode { BO_PREDICT_AUTO = 0, BO_PREDICT_DENSE = 1 } bo_predict_mode;
+/* mode is a bit set: BO_PREDICT_DENSE forces the dense formulation; BO_PREDICT_NO_SEPARABLE
+ * disables the integer-grid fast K* generation (K* = pv * R(f) * T[x_last - c_last], an exp
+ * table over the last grid axis; used only when the candidates are a grid whose last axis is
+ * a multiple of 16 and every training point's last coordinate is an integer on that axis,
+ * checked on the device). */
+typedef enum bo_predict_mode {
+  BO_PREDICT_AUTO = 0,
+  BO_PREDICT_DENSE = 1,
+  BO_PREDICT_NO_SEPARABLE = 2
+} bo_predict_mode;
 
 typedef struct bo_predict_desc {
   int32_t n_obj;              /* objectives (<= BO_MAX_OBJ)                                 */

@@ -67,10 +67,11 @@ def test_predict_vs_reference_golden(bo, name, mode):
             np.testing.assert_array_equal(got.astype(np.float64), ref_sel.astype(np.float64))
 
 
-def test_predict_implicit_grid(bo):
+@pytest.mark.parametrize("mode", ["auto", "dense", "auto-exp", "dense-exp"])
+def test_predict_implicit_grid(bo, mode):
     d = predict_fixture("g1_grid")
     cands = bo.predict.CandidateSet.grid([(0, int(d["grid_shape"][0])), (0, int(d["grid_shape"][1]))])
-    out = _run(bo, d, cands)
+    out = _run(bo, d, cands, mode=mode)
     check_predict(out, d, d["pv"])
     check_topq(out["top_idx"], d["acq"], _excluded(d["cand"], d["x"]), 16)
     np.testing.assert_array_equal(cands.points(out["top_idx"][:3]), d["select_q3"])
@@ -170,8 +171,12 @@ def test_full_size_c3_properties(bo):
     out2 = _run(bo, d, cands, q=16, outputs=("acq",))
     np.testing.assert_array_equal(out["acq"], out2["acq"])
     np.testing.assert_array_equal(out["top_idx"], out2["top_idx"])
-    dense = _run(bo, d, cands, q=16, outputs=("mu", "var", "acq"), mode="dense")
-    check_predict({k: dense[k] for k in ("mu", "var", "acq")}, {k: out[k] for k in ("mu", "var", "acq")}, pv)
+    for mode in ("dense", "auto-exp", "dense-exp"):
+        other = _run(bo, d, cands, q=16, outputs=("mu", "var", "acq"), mode=mode)
+        check_predict({k: other[k] for k in ("mu", "var", "acq")}, {k: out[k] for k in ("mu", "var", "acq")}, pv)
+        check_topq(other["top_idx"], out["acq"], excl, 16)
+    excl = np.zeros(side * side, dtype=bool)
+    excl[lin] = True
     sub = np.sort(rng.choice(side * side, size=4096, replace=False))
     pts = cands.points(sub)
     ref = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv)
