@@ -7,8 +7,8 @@
 //                   unscrambled at the end.  Exactly-zero pivot -> BO_ERR_SINGULAR.
 //   bo_compute_mll  numba_kernels.py:152-235  Gram rebuilt with the trial hyper-parameters
 //                   (update_k), K/pv + 1e-8 I factored by a right-looking blocked Cholesky
-//                   (32x32 blocks: diagonal factor + panel solve in one launch, trailing
-//                   update in a second), then the two triangular solves, log-determinant
+//                   (32x32 blocks: diagonal factor, panel solve and trailing update, one
+//                   launch each), then the two triangular solves, log-determinant
 //                   and the three MLL terms; a non-positive pivot -> BO_ERR_NOT_PD.
 // Both are latency-bound small dense problems (N <= a few thousand); the launches are
 // grid-wide per step so the N x N update spreads over every CU.
@@ -141,30 +141,22 @@ __global__ void corr_kernel(double* __restrict__ dst, const double* __restrict__
   dst[t] = v;
 }
 
-// Factor diagonal block kb (every block does it in LDS) and solve its own row block
-// ib = kb + blockIdx.x: L_ib = A_ib L_kk^-T.  Lower triangle only; in place.
-// The panel solve goes through W = L_kk^-1 (one column per lane, register-resident forward
-// substitution) so the 32 x 32 product X = A_ib W^T runs fully parallel.
-__global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ C, int n, int kb,
+// Factor diagonal block kb in place (one workgroup per objective; unblocked right-looking
+// Cholesky in LDS, LAPACK potf2 order of terms).  Its own launch: the panel solves below read
+// the finished factor, so no workgroup ever sees the block half-written.
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ C, int n, int kb,
                                                          int* __restrict__ status) {
   __shared__ double Lk[NB][NB + 1];
-  __shared__ double Wi[NB][NB + 1];
-  __shared__ double Ab[NB][NB + 1];
-  const int o = blockIdx.y;
+  const int o = blockIdx.x;
   double* c = C + (long long)o * n * n;
   const int k0 = kb * NB;
   const int kn = min(NB, n - k0);
-  const int ib = kb + blockIdx.x;
-  const int i0 = ib * NB;
-  const int in = min(NB, n - i0);
   const int tid = threadIdx.x;
   for (int t = tid; t < NB * NB; t += 256) {
     const int r = t / NB, q = t % NB;
     Lk[r][q] = (r < kn && q < kn && q <= r) ? c[(long long)(k0 + r) * n + k0 + q] : (r == q ? 1.0 : 0.0);
-    if (ib != kb) Ab[r][q] = (r < in && q < kn) ? c[(long long)(i0 + r) * n + k0 + q] : 0.0;
   }
   __syncthreads();
-  // unblocked right-looking Cholesky of the diagonal block (LAPACK potf2 order of terms)
   bool bad = false;
   for (int j = 0; j < kn; ++j) {
     const double d = Lk[j][j];
@@ -180,14 +172,34 @@ __global__ __launch_bounds__(256) void potrf_trsm_kernel(double* __restrict__ C,
     }
     __syncthreads();
   }
-  if (ib == kb) {
-    if (bad && tid == 0) atomicOr(status, 1);
-    for (int t = tid; t < kn * kn; t += 256) {
-      const int r = t / kn, q = t % kn;
-      if (q <= r) c[(long long)(k0 + r) * n + k0 + q] = Lk[r][q];
-    }
-    return;
+  if (bad && tid == 0) atomicOr(status, 1);
+  for (int t = tid; t < kn * kn; t += 256) {
+    const int r = t / kn, q = t % kn;
+    if (q <= r) c[(long long)(k0 + r) * n + k0 + q] = Lk[r][q];
   }
+}
+
+// Panel solve of row block ib = kb + 1 + blockIdx.x: L_ib = A_ib L_kk^-T, reading the factored
+// diagonal block.  Goes through W = L_kk^-1 (one column per lane, register-resident forward
+// substitution) so the 32 x 32 product X = A_ib W^T runs fully parallel.
+__global__ __launch_bounds__(256) void trsm_panel_kernel(double* __restrict__ C, int n, int kb) {
+  __shared__ double Lk[NB][NB + 1];
+  __shared__ double Wi[NB][NB + 1];
+  __shared__ double Ab[NB][NB + 1];
+  const int o = blockIdx.y;
+  double* c = C + (long long)o * n * n;
+  const int k0 = kb * NB;
+  const int kn = min(NB, n - k0);
+  const int ib = kb + 1 + blockIdx.x;
+  const int i0 = ib * NB;
+  const int in = min(NB, n - i0);
+  const int tid = threadIdx.x;
+  for (int t = tid; t < NB * NB; t += 256) {
+    const int r = t / NB, q = t % NB;
+    Lk[r][q] = (r < kn && q < kn && q <= r) ? c[(long long)(k0 + r) * n + k0 + q] : (r == q ? 1.0 : 0.0);
+    Ab[r][q] = (r < in && q < kn) ? c[(long long)(i0 + r) * n + k0 + q] : 0.0;
+  }
+  __syncthreads();
   // W = L_kk^-1: lane `col` forward-substitutes the unit vector e_col (rows >= kn are
   // identity-padded, so W stays well defined for a partial last block)
   if (tid < NB) {
@@ -356,8 +368,10 @@ __attribute__((visibility("hidden"))) int bo_internal_potrf(double* C, int n, in
                                                             int* d_status, hipStream_t s) {
   const int nb = (n + NB - 1) / NB;
   for (int kb = 0; kb < nb; ++kb) {
-    hipLaunchKernelGGL(potrf_trsm_kernel, dim3(nb - kb, n_obj), dim3(256), 0, s, C, n, kb, d_status);
+    hipLaunchKernelGGL(potrf_diag_kernel, dim3(n_obj), dim3(256), 0, s, C, n, kb, d_status);
     const int m = nb - kb - 1;
+    if (m > 0)
+      hipLaunchKernelGGL(trsm_panel_kernel, dim3(m, n_obj), dim3(256), 0, s, C, n, kb);
     if (m > 0)
       hipLaunchKernelGGL(syrk_kernel, dim3(m * (m + 1) / 2, n_obj), dim3(256), 0, s, C, n, kb, nb);
   }

@@ -42,6 +42,11 @@ __device__ unsigned long long g_stamps[4096][8];
 #else
 #define STAMP(var) do { } while (0)
 #endif
+#ifdef BO_ABL_DBGQ
+// Diagnostic build only: triangular-mode accumulators of tile 0 / wave 0 / objective 0.
+__device__ double g_dbgq[64][2][4][64];
+__device__ long long g_dbg_tile;
+#endif
 
 namespace {
 
@@ -133,6 +138,17 @@ __device__ __forceinline__ double kstar_at(const FusedArgs& a, int o, int f, lon
 
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Wait states between the last MFMA of a contraction and the first VALU read of its
+// accumulators.  The compiler's hazard recognizer was observed to under-count them for
+// v_mfma_f64_16x16x4_f64 when the reading block is reached by a branch that skips the
+// previous block (stale accumulator rows, deterministic but data-dependent errors in the
+// triangular variance); 3 x 8 explicit wait states cover the longest f64 MFMA pipeline.
+__device__ __forceinline__ void mfma_drain() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 __device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
@@ -404,11 +420,16 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
           contract_epair<NS, DIM, !MULTI, MULTI && !KMEM>(wr, voff, base, pos, ep, tri, B, wa, wb,
                                                           acc0, acc1, acc2, acc3, sel0, sel1, xs, c, pv, nhl,
                                                           g, nxt);
+          mfma_drain();
 #ifdef BO_ABL_ACC4
           acc0 += acc2;
           acc1 += acc3;
 #endif
           if (tri) {
+#ifdef BO_ABL_DBGQ
+            if (tile == g_dbg_tile && wave == 0 && o == 0 && ep < 64)
+              for (int r = 0; r < 4; ++r) { g_dbgq[ep][0][r][lane] = acc0[r]; g_dbgq[ep][1][r][lane] = acc1[r]; }
+#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               qpart = __builtin_fma(acc0[r], acc0[r], qpart);
@@ -728,7 +749,7 @@ struct KernelTimer {
 
 void timer_mark(hipStream_t s) {
   if (!g_timer.on || g_timer.used >= (int)g_timer.ev.size()) return;
-  hipEventRecord(g_timer.ev[g_timer.used++], s);
+  (void)hipEventRecord(g_timer.ev[g_timer.used++], s);
 }
 
 template <int DIM>
@@ -964,7 +985,7 @@ int bo_update_mean_variance(double* mu, double* var, const double* k_star, int64
 
 int bo_profile_start(int max_launches) {
   if (max_launches < 1) return BO_ERR_ARG;
-  for (auto& e : g_timer.ev) hipEventDestroy(e);
+  for (auto& e : g_timer.ev) (void)hipEventDestroy(e);
   g_timer.ev.assign(2 * (size_t)max_launches, nullptr);
   for (auto& e : g_timer.ev) BO_CHECK_HIP(hipEventCreate(&e));
   g_timer.used = 0;
@@ -992,6 +1013,18 @@ int bo_profile_stop(double* total_ms, int* launches) {
 int bo_debug_stamps(unsigned long long* host, int n_waves) {
   BO_CHECK_HIP(hipDeviceSynchronize());
   BO_CHECK_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * n_waves));
+  return BO_OK;
+}
+#endif
+
+#ifdef BO_ABL_DBGQ
+int bo_debug_set_tile(long long t) {
+  BO_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_tile), &t, sizeof(t)));
+  return BO_OK;
+}
+int bo_debug_dbgq(double* host) {
+  BO_CHECK_HIP(hipDeviceSynchronize());
+  BO_CHECK_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbgq), sizeof(double) * 64 * 2 * 4 * 64));
   return BO_OK;
 }
 #endif

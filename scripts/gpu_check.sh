@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 STEP_OK() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -rf ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -25 gpurun_out/gpu_tests.log
   STEP_OK $rc || exit $rc
 fi

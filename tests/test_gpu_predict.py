@@ -171,16 +171,14 @@ def test_full_size_c3_properties(bo):
     out2 = _run(bo, d, cands, q=16, outputs=("acq",))
     np.testing.assert_array_equal(out["acq"], out2["acq"])
     np.testing.assert_array_equal(out["top_idx"], out2["top_idx"])
+    excl = np.zeros(side * side, dtype=bool)
+    excl[lin] = True
     for mode in ("dense", "auto-exp", "dense-exp"):
         other = _run(bo, d, cands, q=16, outputs=("mu", "var", "acq"), mode=mode)
         check_predict({k: other[k] for k in ("mu", "var", "acq")}, {k: out[k] for k in ("mu", "var", "acq")}, pv)
         check_topq(other["top_idx"], out["acq"], excl, 16)
-    excl = np.zeros(side * side, dtype=bool)
-    excl[lin] = True
     sub = np.sort(rng.choice(side * side, size=4096, replace=False))
     pts = cands.points(sub)
     ref = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv)
     check_predict({k: (out[k][..., sub]) for k in ("mu", "var", "acq")}, ref, pv)
-    excl = np.zeros(side * side, dtype=bool)
-    excl[lin] = True
     check_topq(out["top_idx"], out["acq"], excl, 16)
