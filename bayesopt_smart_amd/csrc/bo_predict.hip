@@ -140,15 +140,25 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Wait states between the last MFMA of a contraction and the first VALU read of its
-// accumulators.  The compiler's hazard recognizer was observed to under-count them for
-// v_mfma_f64_16x16x4_f64 when the reading block is reached by a branch that skips the
-// previous block (stale accumulator rows, deterministic but data-dependent errors in the
-// triangular variance); 3 x 8 explicit wait states cover the longest f64 MFMA pipeline.
-__device__ __forceinline__ void mfma_drain() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
+// Fence between the last MFMA of a contraction and the first read of its accumulators.
+// hipcc's gfx950 hazard recognizer under-counts the wait states a VALU / v_accvgpr_read needs
+// after v_mfma_f64_16x16x4_f64 when the reading block is reached through a branch that skips
+// another block (observed: stale rows of the last MFMA, deterministic data-dependent errors
+// up to 0.15 pv in the triangular variance).  The asm consumes and "redefines" both
+// accumulators in place, so it cannot be scheduled before the MFMAs that produce them and no
+// read of them can be hoisted above it; its 64 wait states cover the MFMA's full latency.
+// AGPR: accumulators allocated in AGPRs (the register-resident kernel) or VGPRs (grid kernel).
+template <bool AGPR, int NOPS = 64>
+__device__ __forceinline__ void mfma_fence(d4& x, d4& y) {
+#define BO_NOPS8 "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+  if (NOPS == 0) {
+    if (AGPR) asm volatile("" : "+a"(x), "+a"(y));
+    else asm volatile("" : "+v"(x), "+v"(y));
+  } else {
+    if (AGPR) asm volatile(BO_NOPS8 : "+a"(x), "+a"(y));
+    else asm volatile(BO_NOPS8 : "+v"(x), "+v"(y));
+  }
+#undef BO_NOPS8
 }
 
 __device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
@@ -252,18 +262,6 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
   const int n_excl = a.excl ? a.n_excl : a.n_train;
   if (a.excl)
     for (int t = tid; t < a.n_excl * DIM; t += blockDim.x) exs_buf[t] = a.excl[t];
-  // separable K* (integer grid, single panel): T_o[m + S - 1] = exp(nhl_o m^2)
-  const bool sep = !MULTI && !KMEM && a.sep_flag &&
-                   __builtin_amdgcn_readfirstlane(*a.sep_flag) == 0;
-  double* tbl = smem + a.off_tbl;
-  double* rw = smem + a.off_rw + wave * a.n_pad * 2;     // [n_pad] x (R, x_last)
-  const int TS = 2 * a.sep_S - 1;
-  if (sep)
-    for (int t = tid; t < a.n_obj * TS; t += blockDim.x) {
-      const int o = t / TS;
-      const double m = (double)(t - o * TS - (a.sep_S - 1));
-      tbl[t] = exp(a.nhl[o] * (m * m));
-    }
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t wr =
@@ -328,45 +326,6 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
         // K* block for this lane: B[s] = K*[f0 + 4s + g][j]  (numba_kernels.py:440-442);
         // padded rows sit at 1e200 so their exp underflows to exactly 0.
         double B[NS];
-        if (sep) {
-          // K*[f][j] = pv exp(nhl |x_f - c_j|^2) = pv * R(f) * T[x_f,last - c_j,last]: the 16
-          // candidates of a wave share every coordinate but the last (one grid row), so the
-          // first factor R(f) = exp(nhl sum_{k != last} (x_fk - c_k)^2) is computed once per
-          // row f by the wave (8 exps per lane at N = 512) and the second is a table lookup.
-          // R is stored negated when that partial distance is 0 (exclusion test below).
-          __syncthreads();                       // rw of the previous objective fully consumed
-          for (int f = lane; f < a.n_pad; f += 64) {
-            const double* r = xs + f * DIM;
-            double sqs = 0.0;
-#pragma unroll
-            for (int k = 0; k < DIM; ++k)
-              if (k != a.dim - 1) { const double d = r[k] - c[k]; sqs = __builtin_fma(d, d, sqs); }
-            double rv = f < a.n_train ? exp(sqs * nhl) : 0.0;
-            if (f < a.n_train && sqs == 0.0) rv = -rv;
-            d2 e;
-            e.x = rv;
-            e.y = f < a.n_train ? r[a.dim - 1] : 0.0;   // last coordinate (integral)
-            ((d2*)rw)[f] = e;
-          }
-          __syncthreads();
-          double cl = 0.0;
-#pragma unroll
-          for (int k = 0; k < DIM; ++k)
-            if (k == a.dim - 1) cl = c[k];
-          const int ci = (int)cl - (a.sep_S - 1);   // index = x_last - c_last + S - 1
-          const double* to = tbl + o * TS;
-#pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            const int f = 4 * s + g;
-            const d2 e = ((const d2*)rw)[f];
-            const int xi = (int)e.y;
-            const int idx = min(max(xi - ci, 0), TS - 1);
-            const double tv = to[idx];
-            B[s] = pv * (fabs(e.x) * tv);
-            if (!a.excl && o == 0) hit = hit || (e.x < 0.0 && xi == (int)cl);
-            if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-          }
-        } else
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const int f = f0 + 4 * s + g;
@@ -420,7 +379,7 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
           contract_epair<NS, DIM, !MULTI, MULTI && !KMEM>(wr, voff, base, pos, ep, tri, B, wa, wb,
                                                           acc0, acc1, acc2, acc3, sel0, sel1, xs, c, pv, nhl,
                                                           g, nxt);
-          mfma_drain();
+          mfma_fence<true>(acc0, acc1);
 #ifdef BO_ABL_ACC4
           acc0 += acc2;
           acc1 += acc3;
@@ -494,6 +453,316 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
     TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
     dst[lane].v = top_v;
     dst[lane].i = top_i;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Chunk-major fused kernel (N <= 512, every candidate kind): the production path.
+//
+// f64 MFMAs and f64 VALU instructions share the SIMD's DP pipe (measured on MI355X: they
+// serialise even across waves), so the time of this kernel is  sum(MFMA) + sum(f64 VALU).
+// The loop order is therefore chosen to generate every K* value exactly ONCE:
+//   for each 32-row chunk c of K* (rows 32c .. 32c+31, 8 values per lane):
+//       generate K*[chunk c][16 candidates]  (B operand, registers)
+//       for each E-pair ep (32 rows of W) that touches chunk c  -- all 16, or ep <= c when
+//       W = R^T is upper triangular:   acc[ep] += W[ep-rows, chunk c] . K*[chunk c]
+// with the accumulators of all (up to 16) E-pairs resident (256 AGPRs, one wave per SIMD).
+// The W stream is packed in exactly this (c, ep, k-step pair) order and streamed from L2
+// through a 4-deep register ring; the next chunk's K* is generated while the current chunk's
+// MFMAs run.  Per 16-MFMA E-pair block there is no VALU work at all.
+//
+// K* generation:
+//   * integer 'ij' grid (bayesian_optimization.py:338-340) whose 16-candidate wave tiles lie
+//     in one grid row (SEP): K*[f][j] = (pv R(f)) * T[x_f,last - c_j,last], R(f) =
+//     exp(nhl sum_{k != last} (x_fk - c_k)^2) computed once per row and wave tile, T the
+//     exp(nhl m^2) table over last-axis differences (LDS); one multiply per value;
+//   * otherwise pv exp(nhl |x_f - c_j|^2) per value (numba_kernels.py:436-442).
+// ---------------------------------------------------------------------------------------
+constexpr int kCMaxEp = 16;              // E-pairs (32 rows each): N <= 512
+
+template <int DIM, bool SEP>
+struct KRows {
+  const double* rv;   // SEP: [n_pad] pv * R(f) (0 for padded rows)
+  const int* rb;      // SEP: [n_pad] table index base x_f,last - c0_last + S - 1
+  const double* tb;   // SEP: objective's table T
+  const double* xs;   // !SEP: training rows [n_pad][DIM] (padded rows at 1e200)
+  double c[DIM];      // !SEP: this lane's candidate
+  double pv, nhl;
+  int jl;
+  __device__ __forceinline__ double at(int f) const {
+    if (SEP) return rv[f] * tb[rb[f] - jl];
+    return pv * exp(sqdist<DIM>(xs, f, c) * nhl);
+  }
+  // the 8 values of 32-row chunk `ch` this lane feeds to the MFMAs: rows 32 ch + 4 s + g
+  __device__ __forceinline__ void chunk(int ch, int g, double (&B)[8]) const {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) B[s] = at(32 * ch + 4 * s + g);
+  }
+};
+
+template <int DIM, bool SEP>
+__device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool tri) {
+  const double* xs = smem;                                  // [n_pad][DIM]
+  const double* alpha = xs + (size_t)a.n_pad * DIM;         // [n_obj][n_pad]
+  const double* exs = alpha + (size_t)a.n_obj * a.n_pad;    // [n_excl][DIM] (explicit set)
+  const double* tbl = smem + a.off_tbl;                     // [n_obj][2S - 1]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, jl = lane & 15;
+  double* rv = smem + a.off_rw + (size_t)wave * a.n_pad * 2;   // per wave: rv[n_pad], rb[n_pad]
+  int* rb = (int*)(rv + a.n_pad);
+  const int TS = 2 * a.sep_S - 1;
+  const int nch = a.n_pad / 32;
+  const int last = a.dim - 1;
+  const int w_obj = a.n_pad * a.n_pad * 8;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
+  const int voff = lane * 16;
+
+  double top_v = -__builtin_inf();
+  long long top_i = -1;
+  for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const long long j = tile * kTile + wave * 16 + jl;
+    const bool valid = j < a.n_cand;
+    double c[DIM];
+    double c0_last = 0.0;
+    if (SEP) {
+      // the wave's 16 candidates: one grid row, consecutive along the last axis
+      const long long j0 = tile * kTile + wave * 16;
+      load_candidate<DIM>(a, j0 < a.n_cand ? j0 : 0, true, c);
+#pragma unroll
+      for (int k = 0; k < DIM; ++k)
+        if (k == last) { c0_last = c[k]; c[k] += (double)jl; }
+    } else {
+      load_candidate<DIM>(a, j, valid, c);
+    }
+    // exclusion (acquisition.py:137-139): an explicit set (or no grid structure) -> compare
+    // coordinates, lane group g checking points g, g+4, ...; the default set on the grid ->
+    // from the row pass below
+    bool hit = false;
+    if (a.excl || !SEP) {
+      const double* es = a.excl ? exs : xs;
+      const int ne = a.excl ? a.n_excl : a.n_train;
+      for (int e = g; e < ne; e += 4) {
+        const double* r = es + e * DIM;
+        bool eq = true;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) eq = eq && (r[k] == c[k]);
+        hit = hit || eq;
+      }
+    }
+    unsigned int xmask = 0;
+    double acq = 0.0;
+    for (int o = 0; o < a.n_obj; ++o) {
+      KRows<DIM, SEP> K;
+      K.rv = rv; K.rb = rb; K.tb = tbl + (size_t)o * TS; K.xs = xs;
+      K.pv = a.pv[o]; K.nhl = a.nhl[o]; K.jl = jl;
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
+      if (SEP) {
+        // row pass: pv R(f) and the table index base of every row (numba_kernels.py:436-442)
+        __builtin_amdgcn_wave_barrier();
+        for (int f = lane; f < a.n_pad; f += 64) {
+          double v = 0.0;
+          int b = a.sep_S - 1 + 15;                          // any in-range index (v = 0)
+          if (f < a.n_train) {
+            const double* r = xs + f * DIM;
+            double sqs = 0.0, xl = 0.0;
+#pragma unroll
+            for (int k = 0; k < DIM; ++k) {
+              if (k == last) xl = r[k];
+              else { const double d = r[k] - c[k]; sqs = __builtin_fma(d, d, sqs); }
+            }
+            v = K.pv * exp(sqs * K.nhl);
+            const int dx = (int)(xl - c0_last);
+            b = dx + a.sep_S - 1;
+            if (o == 0 && sqs == 0.0 && dx >= 0 && dx < 16) xmask |= 1u << dx;
+          }
+          rv[f] = v;
+          rb[f] = b;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      const double* al = alpha + (size_t)o * a.n_pad;
+      const int base = o * w_obj;
+      d2 wa[kPF], wb[kPF];
+      prime_ring(wr, voff, base, wa, wb);
+      int pos = 0;
+      d4 acc[kCMaxEp][2];
+#pragma unroll
+      for (int e = 0; e < kCMaxEp; ++e) {
+        acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
+        acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
+      }
+      double mpart = 0.0;
+      double B[8];
+      K.chunk(0, g, B);
+      for (int ch = 0; ch < nch; ++ch) {
+        double Bn[8];
+        K.chunk(ch + 1 < nch ? ch + 1 : ch, g, Bn);          // next chunk, in the MFMA shadow
+#pragma unroll
+        for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * ch + 4 * s + g], B[s], mpart);
+#pragma unroll
+        for (int e = 0; e < kCMaxEp; ++e) {
+          if (tri ? e <= ch : e < nch) {
+#pragma unroll
+            for (int pp = 0; pp < 4; ++pp) {
+              // MFMAs first, then the refill of the same ring slot (no copy of the operands)
+              acc[e][0] = mfma64(wa[pp].x, B[2 * pp], acc[e][0]);
+              acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
+              acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
+              acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
+              const int so = base + ((pos + kPF) << 11);
+              wa[pp] = wload(wr, voff, so);
+              wb[pp] = wload(wr, voff, so + 1024);
+              ++pos;
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) B[s] = Bn[s];
+      }
+      // q: |v|^2 of every E-pair (triangular) or k . z with the rows 32 ep + g + 4r (+16) of
+      // K* = chunk ep's slots r (4 + r) (dense, numba_kernels.py:525-529)
+      double qpart = 0.0;
+      mfma_fence<true, 64>(acc[0][0], acc[0][1]);
+#pragma unroll
+      for (int e = 0; e < kCMaxEp; ++e) {
+        if (e < nch) {
+          mfma_fence<true, 0>(acc[e][0], acc[e][1]);
+          if (tri) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              qpart = __builtin_fma(acc[e][0][r], acc[e][0][r], qpart);
+              qpart = __builtin_fma(acc[e][1][r], acc[e][1][r], qpart);
+            }
+          } else {
+            double S[8];
+            K.chunk(e, g, S);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              qpart = __builtin_fma(S[r], acc[e][0][r], qpart);
+              qpart = __builtin_fma(S[4 + r], acc[e][1][r], qpart);
+            }
+          }
+        }
+      }
+      qpart += __shfl_xor(qpart, 16, 64);
+      qpart += __shfl_xor(qpart, 32, 64);
+      mpart += __shfl_xor(mpart, 16, 64);
+      mpart += __shfl_xor(mpart, 32, 64);
+      const double pv = a.pv[o], pm = a.pm[o];
+      const double mu = pm + mpart;                                   // :486-488
+      const double var = fmax(pv - qpart, BO_MIN_VARIANCE);           // :532-535
+      const double smu = (mu - pm) / a.rsq_pv[o];                      // :563-565
+      const double svar = var / pv;                                    // :568-570
+      const double u = smu + a.beta[o] * sqrt(fabs(svar));             // acquisition.py:52
+      acq = (o == 0) ? u : acq + u;                                    // acquisition.py:108
+      if (valid && g == 0) {
+        const long long off = (long long)o * a.ld_out + j;
+        if (a.mu) a.mu[off] = mu;
+        if (a.var) a.var[off] = var;
+        if (a.std_mu) a.std_mu[off] = smu;
+        if (a.std_var) a.std_var[off] = svar;
+        if (a.ucb) a.ucb[off] = u;
+      }
+    }
+    if (valid && g == 0 && a.acq) a.acq[j] = acq;
+    if (a.topq > 0) {
+      if (SEP && !a.excl) {
+        // OR the row-pass bits over the wave; bit jl is this lane's candidate
+        unsigned int m = xmask;
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) m |= (unsigned int)__shfl_xor((int)m, sh, 64);
+        hit = (m >> jl) & 1u;
+      }
+      const unsigned long long hb = __ballot(hit);
+      const bool excluded =
+          ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
+      const long long gi = (valid && !excluded) ? a.cand_offset + j : -1;
+      bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+    }
+  }
+  if (a.topq > 0 && lane < a.topq) {
+    TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
+    dst[lane].v = top_v;
+    dst[lane].i = top_i;
+  }
+}
+
+// GRID: the host found the grid structure usable (rows of 16); the device flag then says
+// whether every training point lies on the grid's last axis (sep_check_kernel).
+template <int DIM, bool GRID>
+__global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x;
+  double* xs = smem;
+  double* alpha = xs + (size_t)a.n_pad * DIM;
+  double* exs = alpha + (size_t)a.n_obj * a.n_pad;
+  for (int t = tid; t < a.n_pad * DIM; t += blockDim.x) xs[t] = a.xpad[t];
+  for (int t = tid; t < a.n_obj * a.n_pad; t += blockDim.x) alpha[t] = a.alpha[t];
+  if (a.excl)
+    for (int t = tid; t < a.n_excl * DIM; t += blockDim.x) exs[t] = a.excl[t];
+  const bool sep = GRID && __builtin_amdgcn_readfirstlane(*a.sep_flag) == 0;
+  if (sep) {
+    double* tbl = smem + a.off_tbl;
+    const int TS = 2 * a.sep_S - 1;
+    for (int t = tid; t < a.n_obj * TS; t += blockDim.x) {
+      const int o = t / TS;
+      const double m = (double)(t - o * TS - (a.sep_S - 1));
+      tbl[t] = exp(a.nhl[o] * (m * m));
+    }
+  }
+  __syncthreads();
+  // variance form (set on the device by the K^-1 Cholesky, see predict_impl): uniform
+  const bool tri = a.tri_flag && __builtin_amdgcn_readfirstlane(*a.tri_flag) == 0;
+  if (GRID && sep) cm_tiles<DIM, true>(a, smem, tri);
+  else cm_tiles<DIM, false>(a, smem, tri);
+}
+
+// Pack W (K^-1, or R^T when *tri_flag == 0) into the chunk-major MFMA stream of
+// cm_predict_kernel: per objective, for chunk c, for E-pair ep (all nch, or ep <= c when
+// triangular), for k-step pair pp = 0..3 (k-steps s = 8c + 2pp, +1): the A fragments of
+// E = 2ep and E = 2ep + 1, 64 lanes x 16 B each: {W[16E + (l&15)][4s + (l>>4)], same at s+1}.
+__global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
+                               const double* __restrict__ chol, const int* __restrict__ tri_flag,
+                               int n, int n_pad, int n_obj) {
+  const bool tri = tri_flag && *tri_flag == 0;
+  const int nch = n_pad / 32;
+  const long long pairs = tri ? 4LL * nch * (nch + 1) / 2 : 4LL * nch * nch;
+  const long long per_obj = pairs * 128;                      // d2 entries
+  const long long stride_obj = (long long)n_pad * n_pad / 2;  // d2 entries reserved per objective
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per_obj * n_obj;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(t / per_obj);
+    long long r = t - (long long)o * per_obj;
+    const int lane = (int)(r & 63); r >>= 6;
+    const int which = (int)(r & 1); r >>= 1;
+    const int pp = (int)(r & 3); r >>= 2;
+    // r = pair-block index in (c, ep) order
+    int c, ep;
+    if (tri) {
+      c = (int)((sqrt(8.0 * (double)r + 1.0) - 1.0) * 0.5);
+      while ((long long)(c + 1) * (c + 2) / 2 <= r) ++c;
+      while ((long long)c * (c + 1) / 2 > r) --c;
+      ep = (int)(r - (long long)c * (c + 1) / 2);
+    } else {
+      c = (int)(r / nch);
+      ep = (int)(r - (long long)c * nch);
+    }
+    const int row = 16 * (2 * ep + which) + (lane & 15);
+    const int s = 8 * c + 2 * pp;
+    const int col0 = 4 * s + (lane >> 4), col1 = col0 + 4;
+    d2 v;
+    if (tri) {
+      const double* ro = chol + (long long)o * n * n;   // W[e][f] = R[f][e], f >= e
+      v.x = (row < n && col0 < n && col0 >= row) ? ro[(long long)col0 * n + row] : 0.0;
+      v.y = (row < n && col1 < n && col1 >= row) ? ro[(long long)col1 * n + row] : 0.0;
+    } else {
+      const double* wo = kinv + (long long)o * ld * ld;
+      v.x = (row < n && col0 < n) ? wo[(long long)row * ld + col0] : 0.0;
+      v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
+    }
+    out[(long long)o * stride_obj + (t - (long long)o * per_obj)] = v;
   }
 }
 
@@ -647,9 +916,11 @@ struct Plan {
   bool multi;
   size_t off_alpha, off_xpad, off_excl, off_partial, off_chol, off_status, total;
   bool tri;
-  bool sep;
+  bool cm;               // chunk-major kernel (cm_predict_kernel)
+  bool sep;              // ... with the integer-grid K* generation
   int off_tbl, off_rw;   // LDS offsets in doubles
-  int grid;
+  int grid, waves;       // persistent grid, waves per workgroup
+  long long n_tiles;
   size_t lds;
 };
 
@@ -674,44 +945,62 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   if (d->excl_points && d->n_excl < 0) return BO_ERR_ARG;
   const long long n = d->n_train;
   if (n > (1 << 14)) return BO_ERR_UNSUPPORTED;
-  int n_pad = pad_rows(n);
-  int ns;
-  bool multi = false;
-  if (n_pad <= 32) ns = 8;
-  else if (n_pad <= 64) ns = 16;
-  else if (n_pad <= 128) ns = 32;
-  else if (n_pad <= 256) ns = 64;
-  else if (n_pad <= 384 && !kmem) ns = 96;
-  else if (n_pad <= 512 && !kmem) ns = 128;
-  else { ns = kPanelSteps; multi = true; }   // (materialised-K* path: panels above 256 rows)
-  n_pad = multi ? (int)((n + 511) / 512 * 512) : ns * 4;
-  pl->n_pad = n_pad;
-  pl->ns = ns;
-  pl->multi = multi;
-  pl->n_panels = multi ? n_pad / 512 : 1;
   pl->dim_pad = pad_dim(d->dim);
   pl->n_excl = (int)(d->excl_points ? d->n_excl : n);
-  const size_t lds_base = (size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad +
-                         (d->excl_points ? (size_t)pl->n_excl * pl->dim_pad : 0);
-  pl->lds = lds_base * sizeof(double);
-  if (pl->lds > 160 * 1024) return BO_ERR_UNSUPPORTED;
-  // separable K* for the integer grid (one row per 16-candidate wave tile)
+  const size_t excl_lds = d->excl_points ? (size_t)pl->n_excl * pl->dim_pad : 0;
+  // chunk-major kernel (cm_predict_kernel) for N <= 512; on the reference's 'ij' grid with
+  // 16-aligned rows it generates K* from per-row factors and an exp table (pl->sep)
   pl->sep = false;
+  pl->cm = false;
   pl->off_tbl = pl->off_rw = 0;
-  if (!multi && !kmem && d->cand_kind == BO_CAND_GRID && !(d->mode & BO_PREDICT_NO_SEPARABLE)) {
-    const long long S = d->grid_shape[d->dim - 1];
-    const size_t extra = (size_t)d->n_obj * (2 * S - 1) + (size_t)kWaves * n_pad * 2;
-    if (S % 16 == 0 && S <= 32768 && d->cand_offset % 16 == 0 &&
-        (lds_base + extra) * sizeof(double) <= 160 * 1024) {
-      pl->sep = true;
-      pl->off_tbl = (int)lds_base;
-      pl->off_rw = (int)(lds_base + (size_t)d->n_obj * (2 * S - 1));
-      pl->lds = (lds_base + extra) * sizeof(double);
+  if (!kmem && pad_rows(n) <= 32 * kCMaxEp) {
+    const int n_pad = pad_rows(n);
+    const size_t base = (size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad + excl_lds;
+    pl->cm = true;
+    pl->n_pad = n_pad;
+    pl->ns = n_pad / 4;
+    pl->multi = false;
+    pl->n_panels = 1;
+    pl->lds = base * sizeof(double);
+    if (pl->lds > 160 * 1024) return BO_ERR_UNSUPPORTED;
+    if (d->cand_kind == BO_CAND_GRID && !(d->mode & BO_PREDICT_NO_SEPARABLE)) {
+      const long long S = d->grid_shape[d->dim - 1];
+      const size_t tbl = (size_t)d->n_obj * (2 * S - 1);
+      const size_t lds = base + tbl + (size_t)kWaves * n_pad * 2;
+      if (S % 16 == 0 && S <= 32768 && d->cand_offset % 16 == 0 && lds * sizeof(double) <= 160 * 1024) {
+        pl->sep = true;
+        pl->off_tbl = (int)base;
+        pl->off_rw = (int)(base + tbl);
+        pl->lds = lds * sizeof(double);
+      }
     }
   }
+  if (!pl->cm) {
+    int n_pad = pad_rows(n);
+    int ns;
+    bool multi = false;
+    if (n_pad <= 32) ns = 8;
+    else if (n_pad <= 64) ns = 16;
+    else if (n_pad <= 128) ns = 32;
+    else if (n_pad <= 256) ns = 64;
+    else if (n_pad <= 384 && !kmem) ns = 96;
+    else if (n_pad <= 512 && !kmem) ns = 128;
+    else { ns = kPanelSteps; multi = true; }   // (materialised-K* path: panels above 256 rows)
+    n_pad = multi ? (int)((n + 511) / 512 * 512) : ns * 4;
+    pl->n_pad = n_pad;
+    pl->ns = ns;
+    pl->multi = multi;
+    pl->n_panels = multi ? n_pad / 512 : 1;
+    pl->lds = ((size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad + excl_lds) * sizeof(double);
+    if (pl->lds > 160 * 1024) return BO_ERR_UNSUPPORTED;
+  }
+  const int n_pad = pl->n_pad;
+  const bool multi = pl->multi;
   const size_t w_bytes = (size_t)d->n_obj * n_pad * n_pad * sizeof(double);
   if (w_bytes >= (1ull << 31)) return BO_ERR_UNSUPPORTED;
+  pl->waves = kWaves;
   const long long n_tiles = (d->n_cand + kTile - 1) / kTile;
+  pl->n_tiles = n_tiles;
   const int cus = query_device ? num_cus() : 256;
   pl->grid = (int)(n_tiles < cus ? (n_tiles > 0 ? n_tiles : 1) : cus);
   pl->off_alpha = align256(w_bytes);
@@ -721,7 +1010,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   // partial lists sized for the largest persistent grid any device could use
   pl->off_chol = pl->off_partial +
                  align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry));
-  pl->tri = !multi && !(d->mode & BO_PREDICT_DENSE);
+  pl->tri = !multi && !(d->mode & BO_PREDICT_DENSE);   // (kmem: dense only, see predict_impl)
   pl->off_status = pl->off_chol + (pl->tri ? align256((size_t)d->n_obj * n * n * sizeof(double)) : 0);
   pl->total = pl->off_status + 256 + 256;   // +0: tri status, +16: separable-K* status
   return BO_OK;
@@ -763,6 +1052,18 @@ hipError_t launch_ns(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
     case 96: return launch_fused<96, DIM, false>(fa, pl.grid, pl.lds, s);
     default: return launch_fused<128, DIM, false>(fa, pl.grid, pl.lds, s);
   }
+}
+
+template <int DIM, bool GRID>
+hipError_t launch_cm(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) {
+  auto k = cm_predict_kernel<DIM, GRID>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, fa);
+  return hipGetLastError();
 }
 
 hipError_t launch_kmem(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
@@ -819,7 +1120,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.n_cand = d->n_cand;
   fa.cand_offset = d->cand_offset;
   fa.ld_out = d->ld_out > 0 ? d->ld_out : d->n_cand;
-  fa.n_tiles = (d->n_cand + kTile - 1) / kTile;
+  fa.n_tiles = pl.n_tiles;
   for (int k = 0; k < BO_MAX_DIM; ++k) {
     fa.grid_lo[k] = d->grid_lo[k];
     fa.grid_shape[k] = d->grid_shape[k] > 0 ? d->grid_shape[k] : 1;
@@ -886,8 +1187,12 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     }
     const long long total = (long long)d->n_obj * pl.n_pad * pl.n_pad / 2;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, chol,
-                       fa.tri_flag, (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
+    if (pl.cm)
+      hipLaunchKernelGGL(pack_cm_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, chol,
+                         fa.tri_flag, (int)d->n_train, pl.n_pad, d->n_obj);
+    else
+      hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, chol,
+                         fa.tri_flag, (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
     BO_CHECK_HIP(hipGetLastError());
     const long long rows = (long long)d->n_obj * pl.n_pad;
     hipLaunchKernelGGL(alpha_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, alpha,
@@ -916,6 +1221,12 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   const bool timed = g_timer.on && g_timer.used + 2 <= (int)g_timer.ev.size();
   if (timed) timer_mark(s);
   if (kmem) e = launch_kmem(pl, fa, s);
+  else if (pl.cm) switch (pl.dim_pad) {
+    case 2: e = pl.sep ? launch_cm<2, true>(fa, pl.grid, pl.lds, s) : launch_cm<2, false>(fa, pl.grid, pl.lds, s); break;
+    case 4: e = pl.sep ? launch_cm<4, true>(fa, pl.grid, pl.lds, s) : launch_cm<4, false>(fa, pl.grid, pl.lds, s); break;
+    case 6: e = pl.sep ? launch_cm<6, true>(fa, pl.grid, pl.lds, s) : launch_cm<6, false>(fa, pl.grid, pl.lds, s); break;
+    default: e = pl.sep ? launch_cm<8, true>(fa, pl.grid, pl.lds, s) : launch_cm<8, false>(fa, pl.grid, pl.lds, s); break;
+  }
   else switch (pl.dim_pad) {
     case 2: e = launch_ns<2>(pl, fa, s); break;
     case 4: e = launch_ns<4>(pl, fa, s); break;
@@ -925,7 +1236,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   if (e != hipSuccess) return BO_ERR_HIP;
   if (timed) timer_mark(s);
   if (d->topq > 0) {
-    hipLaunchKernelGGL(topq_merge_kernel, dim3(1), dim3(1024), 0, s, partial, pl.grid * kWaves,
+    hipLaunchKernelGGL(topq_merge_kernel, dim3(1), dim3(1024), 0, s, partial, pl.grid * pl.waves,
                        d->topq, d->top_val, (long long*)d->top_idx);
     BO_CHECK_HIP(hipGetLastError());
   }
