@@ -77,7 +77,7 @@ struct FusedArgs {
   TopEntry* partial;                     // [gridDim.x * kWaves][topq]
   const double* kstar;                   // KMEM: materialised k_star [n_obj][ks_rows][n_cand]
   long long ks_rows;
-  const int* tri_flag;                   // device: 0 => K^-1 = R R^T factored, use R^T (triangular)
+  int upper;                             // cm kernel: W = upper triangle of sym(K^-1), diagonal halved
   // separable K* on an integer grid (see sep_generate): device flag (0 => usable), last-axis
   // extent S and lower bound, LDS offsets (doubles) of the exp tables and per-wave R scratch
   const int* sep_flag;
@@ -160,6 +160,9 @@ __device__ __forceinline__ void mfma_fence(d4& x, d4& y) {
   }
 #undef BO_NOPS8
 }
+
+// vmcnt(n) with expcnt / lgkmcnt left at their maxima (gfx9 s_waitcnt encoding)
+#define BO_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | 0x70 | 0xF00)
 
 __device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
   const int voff = lane * 16;
   // triangular variance formulation (set on the device by the K^-1 Cholesky, see
   // predict_impl); uniform across the grid
-  const bool tri = !MULTI && !KMEM && a.tri_flag && __builtin_amdgcn_readfirstlane(*a.tri_flag) == 0;
+  const bool tri = false;   // (the triangular variance form lives in cm_predict_kernel only)
 
   double top_v = -__builtin_inf();
   long long top_i = -1;
@@ -471,6 +474,12 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
 // through a 4-deep register ring; the next chunk's K* is generated while the current chunk's
 // MFMAs run.  Per 16-MFMA E-pair block there is no VALU work at all.
 //
+// Variance forms (the reference: q = k . (K^-1 k), update_variance numba_kernels.py:521-529):
+//   upper (default): q = 2 k . (U k) with U = upper triangle of sym(K^-1) = (K^-1 + K^-T)/2,
+//     diagonal halved -- exactly k^T K^-1 k in exact arithmetic (k^T A k = k^T sym(A) k), half
+//     the MFMAs, no factorisation;
+//   dense: z = K^-1 k verbatim; q = k . z after the last chunk (chunk ep regenerated).
+//
 // K* generation:
 //   * integer 'ij' grid (bayesian_optimization.py:338-340) whose 16-candidate wave tiles lie
 //     in one grid row (SEP): K*[f][j] = (pv R(f)) * T[x_f,last - c_j,last], R(f) =
@@ -500,8 +509,9 @@ struct KRows {
   }
 };
 
-template <int DIM, bool SEP>
-__device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool tri) {
+template <int DIM, bool SEP, bool UPPER>
+__device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
+  constexpr bool upper = UPPER;
   const double* xs = smem;                                  // [n_pad][DIM]
   const double* alpha = xs + (size_t)a.n_pad * DIM;         // [n_obj][n_pad]
   const double* exs = alpha + (size_t)a.n_obj * a.n_pad;    // [n_excl][DIM] (explicit set)
@@ -520,6 +530,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool 
 
   double top_v = -__builtin_inf();
   long long top_i = -1;
+#ifdef BO_ABL_STAMPS
+  unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_a = 0, t_b = 0;
+  STAMP(t_a);
+#endif
   for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     const long long j = tile * kTile + wave * 16 + jl;
     const bool valid = j < a.n_cand;
@@ -582,6 +597,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool 
         }
         __builtin_amdgcn_wave_barrier();
       }
+#ifdef BO_ABL_STAMPS
+      STAMP(t_b); st_sum[0] += t_b - t_a; t_a = t_b;   // tile setup + row pass
+#endif
       const double* al = alpha + (size_t)o * a.n_pad;
       const int base = o * w_obj;
       d2 wa[kPF], wb[kPF];
@@ -593,17 +611,18 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool 
         acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
         acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
       }
-      double mpart = 0.0;
-      double B[8];
-      K.chunk(0, g, B);
-      for (int ch = 0; ch < nch; ++ch) {
-        double Bn[8];
-        K.chunk(ch + 1 < nch ? ch + 1 : ch, g, Bn);          // next chunk, in the MFMA shadow
+      double mpart = 0.0, qpart = 0.0;
+      // one chunk: MFMAs from register set B while the next chunk's K* is generated into Bn
+      // (the two sets alternate: no register copies between the chunks)
+      auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8]) {
+        if (ch + 1 < nch) K.chunk(ch + 1, g, Bn);             // next chunk, in the MFMA shadow
 #pragma unroll
         for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * ch + 4 * s + g], B[s], mpart);
+        // E-pairs touching chunk ch, in ascending order: ep <= ch (upper) or all (a prefix of
+        // the unrolled sequence either way, which keeps hipcc's counted vmcnt waits exact)
 #pragma unroll
         for (int e = 0; e < kCMaxEp; ++e) {
-          if (tri ? e <= ch : e < nch) {
+          if (upper ? e <= ch : e < nch) {
 #pragma unroll
             for (int pp = 0; pp < 4; ++pp) {
               // MFMAs first, then the refill of the same ring slot (no copy of the operands)
@@ -612,40 +631,46 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool 
               acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
               acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
               const int so = base + ((pos + kPF) << 11);
+#ifndef BO_ABL_NOLOAD
               wa[pp] = wload(wr, voff, so);
               wb[pp] = wload(wr, voff, so + 1024);
+#else   // ablation build only: no W stream (operands stay in the ring)
+              asm volatile("" : "+v"(wa[pp]), "+v"(wb[pp]) : "s"(so));
+#endif
               ++pos;
             }
           }
         }
-#pragma unroll
-        for (int s = 0; s < 8; ++s) B[s] = Bn[s];
+      };
+      double BX[8], BY[8];
+      K.chunk(0, g, BX);
+      int ch = 0;
+      for (; ch + 1 < nch; ch += 2) {
+        chunk_step(ch, BX, BY);
+        chunk_step(ch + 1, BY, BX);
       }
-      // q: |v|^2 of every E-pair (triangular) or k . z with the rows 32 ep + g + 4r (+16) of
-      // K* = chunk ep's slots r (4 + r) (dense, numba_kernels.py:525-529)
-      double qpart = 0.0;
-      mfma_fence<true, 64>(acc[0][0], acc[0][1]);
+      if (ch < nch) chunk_step(ch, BX, BY);
+      // q = k . z (dense) or 2 k . (U k) (upper) with the rows 32 ep + g + 4r (+16) of K* =
+      // chunk ep's slots r (4 + r), regenerated here (no branch inside the MFMA stream: a
+      // branch join there costs a vmcnt(0) drain of the W ring).  A full fence per
+      // accumulator: the scheduler may sink any E-pair's last MFMAs down to its own fence.
 #pragma unroll
       for (int e = 0; e < kCMaxEp; ++e) {
         if (e < nch) {
-          mfma_fence<true, 0>(acc[e][0], acc[e][1]);
-          if (tri) {
+          mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+          double S[8];
+          K.chunk(e, g, S);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              qpart = __builtin_fma(acc[e][0][r], acc[e][0][r], qpart);
-              qpart = __builtin_fma(acc[e][1][r], acc[e][1][r], qpart);
-            }
-          } else {
-            double S[8];
-            K.chunk(e, g, S);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              qpart = __builtin_fma(S[r], acc[e][0][r], qpart);
-              qpart = __builtin_fma(S[4 + r], acc[e][1][r], qpart);
-            }
+          for (int r = 0; r < 4; ++r) {
+            qpart = __builtin_fma(S[r], acc[e][0][r], qpart);
+            qpart = __builtin_fma(S[4 + r], acc[e][1][r], qpart);
           }
         }
       }
+      if (upper) qpart *= 2.0;
+#ifdef BO_ABL_STAMPS
+      STAMP(t_b); st_sum[1] += t_b - t_a; t_a = t_b;   // chunk loop (MFMAs) + epilogue
+#endif
       qpart += __shfl_xor(qpart, 16, 64);
       qpart += __shfl_xor(qpart, 32, 64);
       mpart += __shfl_xor(mpart, 16, 64);
@@ -682,6 +707,15 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool 
       bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
     }
   }
+  BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
+#ifdef BO_ABL_STAMPS
+  STAMP(t_b); st_sum[3] += t_b - t_a;
+  if (lane == 0) {
+    const int w = blockIdx.x * kWaves + wave;
+    for (int k = 0; k < 4; ++k) g_stamps[w][k] = st_sum[k];
+    g_stamps[w][4] = 1;
+  }
+#endif
   if (a.topq > 0 && lane < a.topq) {
     TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
     dst[lane].v = top_v;
@@ -691,7 +725,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem, bool 
 
 // GRID: the host found the grid structure usable (rows of 16); the device flag then says
 // whether every training point lies on the grid's last axis (sep_check_kernel).
-template <int DIM, bool GRID>
+template <int DIM, bool GRID, bool UPPER>
 __global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x;
@@ -713,22 +747,20 @@ __global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
     }
   }
   __syncthreads();
-  // variance form (set on the device by the K^-1 Cholesky, see predict_impl): uniform
-  const bool tri = a.tri_flag && __builtin_amdgcn_readfirstlane(*a.tri_flag) == 0;
-  if (GRID && sep) cm_tiles<DIM, true>(a, smem, tri);
-  else cm_tiles<DIM, false>(a, smem, tri);
+  if (GRID && sep) cm_tiles<DIM, true, UPPER>(a, smem);
+  else cm_tiles<DIM, false, UPPER>(a, smem);
 }
 
-// Pack W (K^-1, or R^T when *tri_flag == 0) into the chunk-major MFMA stream of
-// cm_predict_kernel: per objective, for chunk c, for E-pair ep (all nch, or ep <= c when
-// triangular), for k-step pair pp = 0..3 (k-steps s = 8c + 2pp, +1): the A fragments of
-// E = 2ep and E = 2ep + 1, 64 lanes x 16 B each: {W[16E + (l&15)][4s + (l>>4)], same at s+1}.
+// Pack W into the chunk-major MFMA stream of cm_predict_kernel: per objective, for chunk c
+// ascending, for E-pair ep ascending (ep <= c when upper, all otherwise),
+// for k-step pair pp = 0..3 (k-steps s = 8c + 2pp, +1): the A fragments of E = 2ep and
+// E = 2ep + 1, 64 lanes x 16 B each: {W[16E + (l&15)][4s + (l>>4)], same at s+1}.
+//   dense: W = K^-1 (leading dim ld);
+//   upper: W[e][f] = (K^-1[e][f] + K^-1[f][e]) / 2 for f > e, K^-1[e][e] / 2 for f == e, else 0.
 __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
-                               const double* __restrict__ chol, const int* __restrict__ tri_flag,
-                               int n, int n_pad, int n_obj) {
-  const bool tri = tri_flag && *tri_flag == 0;
+                               int upper, int n, int n_pad, int n_obj) {
   const int nch = n_pad / 32;
-  const long long pairs = tri ? 4LL * nch * (nch + 1) / 2 : 4LL * nch * nch;
+  const long long pairs = upper ? 4LL * nch * (nch + 1) / 2 : 4LL * nch * nch;
   const long long per_obj = pairs * 128;                      // d2 entries
   const long long stride_obj = (long long)n_pad * n_pad / 2;  // d2 entries reserved per objective
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per_obj * n_obj;
@@ -738,13 +770,15 @@ __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ 
     const int lane = (int)(r & 63); r >>= 6;
     const int which = (int)(r & 1); r >>= 1;
     const int pp = (int)(r & 3); r >>= 2;
-    // r = pair-block index in (c, ep) order
+    // r = block index in the (c ascending, ep ascending) order
     int c, ep;
-    if (tri) {
-      c = (int)((sqrt(8.0 * (double)r + 1.0) - 1.0) * 0.5);
-      while ((long long)(c + 1) * (c + 2) / 2 <= r) ++c;
-      while ((long long)c * (c + 1) / 2 > r) --c;
-      ep = (int)(r - (long long)c * (c + 1) / 2);
+    if (upper) {
+      // chunk c holds c + 1 blocks (ep = 0..c); blocks before it: T(c) = c(c+1)/2
+      int cc = (int)((sqrt(8.0 * (double)r + 1.0) - 1.0) * 0.5);
+      while ((long long)(cc + 1) * (cc + 2) / 2 <= r) ++cc;
+      while ((long long)cc * (cc + 1) / 2 > r) --cc;
+      c = cc;
+      ep = (int)(r - (long long)cc * (cc + 1) / 2);
     } else {
       c = (int)(r / nch);
       ep = (int)(r - (long long)c * nch);
@@ -752,16 +786,17 @@ __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ 
     const int row = 16 * (2 * ep + which) + (lane & 15);
     const int s = 8 * c + 2 * pp;
     const int col0 = 4 * s + (lane >> 4), col1 = col0 + 4;
+    const double* wo = kinv + (long long)o * ld * ld;
+    auto w = [&](int e, int f) -> double {
+      if (e >= n || f >= n) return 0.0;
+      if (!upper) return wo[(long long)e * ld + f];
+      if (f < e) return 0.0;
+      if (f == e) return 0.5 * wo[(long long)e * ld + e];
+      return 0.5 * (wo[(long long)e * ld + f] + wo[(long long)f * ld + e]);
+    };
     d2 v;
-    if (tri) {
-      const double* ro = chol + (long long)o * n * n;   // W[e][f] = R[f][e], f >= e
-      v.x = (row < n && col0 < n && col0 >= row) ? ro[(long long)col0 * n + row] : 0.0;
-      v.y = (row < n && col1 < n && col1 >= row) ? ro[(long long)col1 * n + row] : 0.0;
-    } else {
-      const double* wo = kinv + (long long)o * ld * ld;
-      v.x = (row < n && col0 < n) ? wo[(long long)row * ld + col0] : 0.0;
-      v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
-    }
+    v.x = w(row, col0);
+    v.y = w(row, col1);
     out[(long long)o * stride_obj + (t - (long long)o * per_obj)] = v;
   }
 }
@@ -788,17 +823,11 @@ __global__ void pad_points_kernel(double* __restrict__ out, const double* __rest
   out[t] = r < rows ? (k < dim ? in[r * dim + k] : 0.0) : fill;
 }
 
-// Pack the A operand of the contraction into MFMA fragment order, zero padded.
-// Element (ep, pair, which, lane) of panel `panel` holds W[16E + (l&15)][4s + (l>>4)] and the
-// same at s+1 (E = 2ep + which, s = panel*ns_panel + 2*pair):
-//   dense:      W = K^-1 (row-major, leading dim ld); stream index = (panel, ep, pair)
-//   triangular: W = R^T with K^-1 = R R^T (R lower, dense n x n in `chol`), W[e][f] = R[f][e]
-//               for f >= e; only pairs >= 4ep are stored, stream index = off(ep) + pair - 4ep.
-// The choice is made on the device: triangular iff *tri_flag == 0 (Cholesky succeeded).
+// Pack K^-1 into the MFMA fragment order of fused_predict_kernel (N > 512 panels and the
+// materialised-K* path), zero padded.  Element (panel, ep, pair, which, lane) holds
+// W[16E + (l&15)][4s + (l>>4)] and the same at s+1 (E = 2ep + which, s = panel*ns_panel + 2*pair).
 __global__ void pack_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
-                            const double* __restrict__ chol, const int* __restrict__ tri_flag,
                             int n, int n_pad, int ns_panel, int n_obj) {
-  const bool tri = tri_flag && *tri_flag == 0;
   const long long per_obj = (long long)n_pad * n_pad / 2;
   const long long total = per_obj * n_obj;
   const int n_ep = n_pad / 32;
@@ -815,34 +844,12 @@ __global__ void pack_kernel(d2* __restrict__ out, const double* __restrict__ kin
     const int row = 16 * (2 * ep + which) + (lane & 15);
     const int s = panel * ns_panel + 2 * pair;
     const int col0 = 4 * s + (lane >> 4), col1 = col0 + 4;
+    const double* wo = kinv + (long long)o * ld * ld;
     d2 v;
-    long long dst = t;
-    if (tri) {
-      if (pair < 4 * ep) continue;
-      const long long off = (long long)ep * npair - 2LL * ep * (ep - 1);   // sum_{e<ep} (npair - 4e)
-      dst = (long long)o * per_obj + ((off + pair - 4 * ep) * 2 + which) * 64 + lane;
-      const double* ro = chol + (long long)o * n * n;
-      v.x = (row < n && col0 < n && col0 >= row) ? ro[(long long)col0 * n + row] : 0.0;
-      v.y = (row < n && col1 < n && col1 >= row) ? ro[(long long)col1 * n + row] : 0.0;
-    } else {
-      const double* wo = kinv + (long long)o * ld * ld;
-      v.x = (row < n && col0 < n) ? wo[(long long)row * ld + col0] : 0.0;
-      v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
-    }
-    out[dst] = v;
+    v.x = (row < n && col0 < n) ? wo[(long long)row * ld + col0] : 0.0;
+    v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
+    out[t] = v;
   }
-}
-
-// dense n x n copy of K^-1's leading block (the Cholesky input)
-__global__ void copy_square_kernel(double* __restrict__ dst, const double* __restrict__ src,
-                                   long long ld, int n, int n_obj) {
-  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  const long long per = (long long)n * n;
-  if (t >= per * n_obj) return;
-  const int o = (int)(t / per);
-  const long long r = t - o * per;
-  const int i = (int)(r / n), j = (int)(r - (long long)i * n);
-  dst[t] = src[(long long)o * ld * ld + (long long)i * ld + j];
 }
 
 // alpha[o][f] = sum_e Kinv[o][f][e] * (y[e][o] - pm[o])   (numba_kernels.py:477-483),
@@ -915,7 +922,6 @@ struct Plan {
   int n_pad, ns, n_panels, dim_pad, n_excl;
   bool multi;
   size_t off_alpha, off_xpad, off_excl, off_partial, off_chol, off_status, total;
-  bool tri;
   bool cm;               // chunk-major kernel (cm_predict_kernel)
   bool sep;              // ... with the integer-grid K* generation
   int off_tbl, off_rw;   // LDS offsets in doubles
@@ -1010,8 +1016,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   // partial lists sized for the largest persistent grid any device could use
   pl->off_chol = pl->off_partial +
                  align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry));
-  pl->tri = !multi && !(d->mode & BO_PREDICT_DENSE);   // (kmem: dense only, see predict_impl)
-  pl->off_status = pl->off_chol + (pl->tri ? align256((size_t)d->n_obj * n * n * sizeof(double)) : 0);
+  pl->off_status = pl->off_chol;
   pl->total = pl->off_status + 256 + 256;   // +0: tri status, +16: separable-K* status
   return BO_OK;
 }
@@ -1054,9 +1059,9 @@ hipError_t launch_ns(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
   }
 }
 
-template <int DIM, bool GRID>
-hipError_t launch_cm(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) {
-  auto k = cm_predict_kernel<DIM, GRID>;
+template <int DIM, bool GRID, bool UPPER>
+hipError_t launch_cm_k(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) {
+  auto k = cm_predict_kernel<DIM, GRID, UPPER>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
@@ -1064,6 +1069,15 @@ hipError_t launch_cm(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) 
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, fa);
   return hipGetLastError();
+}
+
+template <int DIM>
+hipError_t launch_cm(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  if (fa.upper)
+    return pl.sep ? launch_cm_k<DIM, true, true>(fa, pl.grid, pl.lds, st)
+                  : launch_cm_k<DIM, false, true>(fa, pl.grid, pl.lds, st);
+  return pl.sep ? launch_cm_k<DIM, true, false>(fa, pl.grid, pl.lds, st)
+                : launch_cm_k<DIM, false, false>(fa, pl.grid, pl.lds, st);
 }
 
 hipError_t launch_kmem(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
@@ -1157,10 +1171,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.kstar = kstar;
   fa.ks_rows = ks_rows;
 
-  const bool tri = pl.tri && !kmem;
-  double* chol = (double*)(ws + pl.off_chol);
-  int* tri_flag = (int*)(ws + pl.off_status);
-  fa.tri_flag = tri ? tri_flag : nullptr;
+  fa.upper = (pl.cm && !(d->mode & BO_PREDICT_DENSE)) ? 1 : 0;
   int* sep_flag = (int*)(ws + pl.off_status + 16);
   fa.sep_flag = pl.sep ? sep_flag : nullptr;
   fa.sep_S = pl.sep ? (int)d->grid_shape[d->dim - 1] : 1;
@@ -1174,25 +1185,14 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     BO_CHECK_HIP(hipGetLastError());
   }
   {
-    if (tri) {
-      // K^-1 = R R^T on the device; a failed factorisation leaves *tri_flag = 1 and every
-      // later kernel of this call takes the dense formulation
-      BO_CHECK_HIP(hipMemsetAsync(tri_flag, 0, sizeof(int), s));
-      const long long nn = (long long)d->n_obj * d->n_train * d->n_train;
-      hipLaunchKernelGGL(copy_square_kernel, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s,
-                         chol, d->kinv, d->ld_k, (int)d->n_train, d->n_obj);
-      BO_CHECK_HIP(hipGetLastError());
-      const int pst = bo_internal_potrf(chol, (int)d->n_train, d->n_obj, tri_flag, s);
-      if (pst != BO_OK) return pst;
-    }
     const long long total = (long long)d->n_obj * pl.n_pad * pl.n_pad / 2;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     if (pl.cm)
-      hipLaunchKernelGGL(pack_cm_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, chol,
-                         fa.tri_flag, (int)d->n_train, pl.n_pad, d->n_obj);
+      hipLaunchKernelGGL(pack_cm_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, fa.upper,
+                         (int)d->n_train, pl.n_pad, d->n_obj);
     else
-      hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, chol,
-                         fa.tri_flag, (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
+      hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k,
+                         (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
     BO_CHECK_HIP(hipGetLastError());
     const long long rows = (long long)d->n_obj * pl.n_pad;
     hipLaunchKernelGGL(alpha_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, alpha,
@@ -1222,10 +1222,10 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   if (timed) timer_mark(s);
   if (kmem) e = launch_kmem(pl, fa, s);
   else if (pl.cm) switch (pl.dim_pad) {
-    case 2: e = pl.sep ? launch_cm<2, true>(fa, pl.grid, pl.lds, s) : launch_cm<2, false>(fa, pl.grid, pl.lds, s); break;
-    case 4: e = pl.sep ? launch_cm<4, true>(fa, pl.grid, pl.lds, s) : launch_cm<4, false>(fa, pl.grid, pl.lds, s); break;
-    case 6: e = pl.sep ? launch_cm<6, true>(fa, pl.grid, pl.lds, s) : launch_cm<6, false>(fa, pl.grid, pl.lds, s); break;
-    default: e = pl.sep ? launch_cm<8, true>(fa, pl.grid, pl.lds, s) : launch_cm<8, false>(fa, pl.grid, pl.lds, s); break;
+    case 2: e = launch_cm<2>(pl, fa, s); break;
+    case 4: e = launch_cm<4>(pl, fa, s); break;
+    case 6: e = launch_cm<6>(pl, fa, s); break;
+    default: e = launch_cm<8>(pl, fa, s); break;
   }
   else switch (pl.dim_pad) {
     case 2: e = launch_ns<2>(pl, fa, s); break;

@@ -24,8 +24,8 @@ for mode in sys.argv[1:] or ["auto"]:
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
     fn(buf, 4096)
     a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8)
-    a = a[a[:, 4] > 0][:, :5].astype(np.float64)
-    names = ["cand+excl", "K* gen (exp)", "contraction", "epilogue/stores", "topq+loop"]
+    a = a[a[:, 4] > 0][:, :4].astype(np.float64)
+    names = ["setup+row pass", "chunk loop", "epilogue q", "outputs/topq/rest"]
     tot = a.sum(1).mean()
     print(mode, "waves", a.shape[0], "cycles/wave", f"{tot:.4g}",
           {n: f"{v / tot * 100:.1f}%" for n, v in zip(names, a.mean(0))})
