@@ -605,65 +605,74 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       d2 wa[kPF], wb[kPF];
       prime_ring(wr, voff, base, wa, wb);
       int pos = 0;
-      d4 acc[kCMaxEp][2];
-#pragma unroll
-      for (int e = 0; e < kCMaxEp; ++e) {
-        acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
-        acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
-      }
       double mpart = 0.0, qpart = 0.0;
-      // one chunk: MFMAs from register set B while the next chunk's K* is generated into Bn
-      // (the two sets alternate: no register copies between the chunks)
-      auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8]) {
-        if (ch + 1 < nch) K.chunk(ch + 1, g, Bn);             // next chunk, in the MFMA shadow
-#pragma unroll
-        for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * ch + 4 * s + g], B[s], mpart);
-        // E-pairs touching chunk ch, in ascending order: ep <= ch (upper) or all (a prefix of
-        // the unrolled sequence either way, which keeps hipcc's counted vmcnt waits exact)
+      d4 acc[kCMaxEp][2];
+      // E-pairs in groups of kCMaxEp (the accumulators one wave holds: 512 rows); a group
+      // streams the chunks that touch it (c >= its first E-pair when upper, all otherwise) and
+      // regenerates their K*.  One group when N <= 512.
+      for (int e0 = 0; e0 < nch; e0 += kCMaxEp) {
+        const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
 #pragma unroll
         for (int e = 0; e < kCMaxEp; ++e) {
-          if (upper ? e <= ch : e < nch) {
+          acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
+          acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
+        }
+        // one chunk: MFMAs from register set B while the next chunk's K* is generated into
+        // Bn (the two sets alternate: no register copies between the chunks)
+        auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8]) {
+          if (ch + 1 < nch) K.chunk(ch + 1, g, Bn);             // next chunk, in the MFMA shadow
+          if (e0 == 0) {
 #pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-              // MFMAs first, then the refill of the same ring slot (no copy of the operands)
-              acc[e][0] = mfma64(wa[pp].x, B[2 * pp], acc[e][0]);
-              acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
-              acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
-              acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
-              const int so = base + ((pos + kPF) << 11);
+            for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * ch + 4 * s + g], B[s], mpart);
+          }
+          // the group's E-pairs touching chunk ch, ascending: e0 + e <= ch (upper) or all (a
+          // prefix of the unrolled sequence either way, which keeps hipcc's vmcnt waits exact)
+#pragma unroll
+          for (int e = 0; e < kCMaxEp; ++e) {
+            if (e < eN && (!upper || e0 + e <= ch)) {
+#pragma unroll
+              for (int pp = 0; pp < 4; ++pp) {
+                // MFMAs first, then the refill of the same ring slot (no operand copies)
+                acc[e][0] = mfma64(wa[pp].x, B[2 * pp], acc[e][0]);
+                acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
+                acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
+                acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
+                const int so = base + ((pos + kPF) << 11);
 #ifndef BO_ABL_NOLOAD
-              wa[pp] = wload(wr, voff, so);
-              wb[pp] = wload(wr, voff, so + 1024);
+                wa[pp] = wload(wr, voff, so);
+                wb[pp] = wload(wr, voff, so + 1024);
 #else   // ablation build only: no W stream (operands stay in the ring)
-              asm volatile("" : "+v"(wa[pp]), "+v"(wb[pp]) : "s"(so));
+                asm volatile("" : "+v"(wa[pp]), "+v"(wb[pp]) : "s"(so));
 #endif
-              ++pos;
+                ++pos;
+              }
             }
           }
+        };
+        const int c0 = upper ? e0 : 0;
+        double BX[8], BY[8];
+        K.chunk(c0, g, BX);
+        int ch = c0;
+        for (; ch + 1 < nch; ch += 2) {
+          chunk_step(ch, BX, BY);
+          chunk_step(ch + 1, BY, BX);
         }
-      };
-      double BX[8], BY[8];
-      K.chunk(0, g, BX);
-      int ch = 0;
-      for (; ch + 1 < nch; ch += 2) {
-        chunk_step(ch, BX, BY);
-        chunk_step(ch + 1, BY, BX);
-      }
-      if (ch < nch) chunk_step(ch, BX, BY);
-      // q = k . z (dense) or 2 k . (U k) (upper) with the rows 32 ep + g + 4r (+16) of K* =
-      // chunk ep's slots r (4 + r), regenerated here (no branch inside the MFMA stream: a
-      // branch join there costs a vmcnt(0) drain of the W ring).  A full fence per
-      // accumulator: the scheduler may sink any E-pair's last MFMAs down to its own fence.
+        if (ch < nch) chunk_step(ch, BX, BY);
+        // q = k . z (dense) or 2 k . (U k) (upper) with the rows 32 ep + g + 4r (+16) of K* =
+        // chunk ep's slots r (4 + r), regenerated here (no branch inside the MFMA stream: a
+        // branch join there costs a vmcnt(0) drain of the W ring).  A full fence per
+        // accumulator: the scheduler may sink any E-pair's last MFMAs down to its own fence.
 #pragma unroll
-      for (int e = 0; e < kCMaxEp; ++e) {
-        if (e < nch) {
-          mfma_fence<true, 64>(acc[e][0], acc[e][1]);
-          double S[8];
-          K.chunk(e, g, S);
+        for (int e = 0; e < kCMaxEp; ++e) {
+          if (e < eN) {
+            mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+            double S[8];
+            K.chunk(e0 + e, g, S);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            qpart = __builtin_fma(S[r], acc[e][0][r], qpart);
-            qpart = __builtin_fma(S[4 + r], acc[e][1][r], qpart);
+            for (int r = 0; r < 4; ++r) {
+              qpart = __builtin_fma(S[r], acc[e][0][r], qpart);
+              qpart = __builtin_fma(S[4 + r], acc[e][1][r], qpart);
+            }
           }
         }
       }
@@ -751,17 +760,26 @@ __global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
   else cm_tiles<DIM, false, UPPER>(a, smem);
 }
 
-// Pack W into the chunk-major MFMA stream of cm_predict_kernel: per objective, for chunk c
-// ascending, for E-pair ep ascending (ep <= c when upper, all otherwise),
+// Pack W into the chunk-major MFMA stream of cm_predict_kernel: per objective, for each group of
+// kCMaxEp E-pairs, for chunk c ascending (from the group's first E-pair when upper), for the
+// group's E-pairs ep ascending (ep <= c when upper),
 // for k-step pair pp = 0..3 (k-steps s = 8c + 2pp, +1): the A fragments of E = 2ep and
 // E = 2ep + 1, 64 lanes x 16 B each: {W[16E + (l&15)][4s + (l>>4)], same at s+1}.
 //   dense: W = K^-1 (leading dim ld);
 //   upper: W[e][f] = (K^-1[e][f] + K^-1[f][e]) / 2 for f > e, K^-1[e][e] / 2 for f == e, else 0.
+__device__ __forceinline__ long long cm_group_blocks(int nch, int e0, int upper) {
+  const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
+  if (!upper) return (long long)nch * eN;
+  // chunks e0 .. e0+eN-2 hold 1 .. eN-1 blocks, the nch - e0 - eN + 1 later ones eN each
+  return (long long)(eN - 1) * eN / 2 + (long long)(nch - e0 - eN + 1) * eN;
+}
+
 __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
                                int upper, int n, int n_pad, int n_obj) {
   const int nch = n_pad / 32;
-  const long long pairs = upper ? 4LL * nch * (nch + 1) / 2 : 4LL * nch * nch;
-  const long long per_obj = pairs * 128;                      // d2 entries
+  long long blocks = 0;
+  for (int e0 = 0; e0 < nch; e0 += kCMaxEp) blocks += cm_group_blocks(nch, e0, upper);
+  const long long per_obj = blocks * 512;                     // d2 entries (4 pairs x 2 x 64)
   const long long stride_obj = (long long)n_pad * n_pad / 2;  // d2 entries reserved per objective
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per_obj * n_obj;
        t += (long long)gridDim.x * blockDim.x) {
@@ -770,19 +788,30 @@ __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ 
     const int lane = (int)(r & 63); r >>= 6;
     const int which = (int)(r & 1); r >>= 1;
     const int pp = (int)(r & 3); r >>= 2;
-    // r = block index in the (c ascending, ep ascending) order
-    int c, ep;
-    if (upper) {
-      // chunk c holds c + 1 blocks (ep = 0..c); blocks before it: T(c) = c(c+1)/2
-      int cc = (int)((sqrt(8.0 * (double)r + 1.0) - 1.0) * 0.5);
-      while ((long long)(cc + 1) * (cc + 2) / 2 <= r) ++cc;
-      while ((long long)cc * (cc + 1) / 2 > r) --cc;
-      c = cc;
-      ep = (int)(r - (long long)cc * (cc + 1) / 2);
-    } else {
-      c = (int)(r / nch);
-      ep = (int)(r - (long long)c * nch);
+    // r = block index: groups of kCMaxEp E-pairs in order; within a group chunks c
+    // ascending, within a chunk the group's E-pairs ascending (ep <= c when upper)
+    int e0 = 0;
+    for (;; e0 += kCMaxEp) {
+      const long long nb = cm_group_blocks(nch, e0, upper);
+      if (r < nb) break;
+      r -= nb;
     }
+    const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
+    int c, el;
+    if (!upper) {
+      c = (int)(r / eN);
+      el = (int)(r % eN);
+    } else if (r < (long long)(eN - 1) * eN / 2) {           // partial chunks: 1, 2, ... blocks
+      int sz = 1;
+      while (r >= sz) { r -= sz; ++sz; }
+      c = e0 + sz - 1;
+      el = (int)r;
+    } else {
+      r -= (long long)(eN - 1) * eN / 2;
+      c = e0 + eN - 1 + (int)(r / eN);
+      el = (int)(r % eN);
+    }
+    const int ep = e0 + el;
     const int row = 16 * (2 * ep + which) + (lane & 15);
     const int s = 8 * c + 2 * pp;
     const int col0 = 4 * s + (lane >> 4), col1 = col0 + 4;
@@ -959,7 +988,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   pl->sep = false;
   pl->cm = false;
   pl->off_tbl = pl->off_rw = 0;
-  if (!kmem && pad_rows(n) <= 32 * kCMaxEp) {
+  if (!kmem) {
     const int n_pad = pad_rows(n);
     const size_t base = (size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad + excl_lds;
     pl->cm = true;
@@ -1044,19 +1073,6 @@ struct KernelTimer {
 void timer_mark(hipStream_t s) {
   if (!g_timer.on || g_timer.used >= (int)g_timer.ev.size()) return;
   (void)hipEventRecord(g_timer.ev[g_timer.used++], s);
-}
-
-template <int DIM>
-hipError_t launch_ns(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
-  if (pl.multi) return launch_fused<kPanelSteps, DIM, true>(fa, pl.grid, pl.lds, s);
-  switch (pl.ns) {
-    case 8: return launch_fused<8, DIM, false>(fa, pl.grid, pl.lds, s);
-    case 16: return launch_fused<16, DIM, false>(fa, pl.grid, pl.lds, s);
-    case 32: return launch_fused<32, DIM, false>(fa, pl.grid, pl.lds, s);
-    case 64: return launch_fused<64, DIM, false>(fa, pl.grid, pl.lds, s);
-    case 96: return launch_fused<96, DIM, false>(fa, pl.grid, pl.lds, s);
-    default: return launch_fused<128, DIM, false>(fa, pl.grid, pl.lds, s);
-  }
 }
 
 template <int DIM, bool GRID, bool UPPER>
@@ -1227,12 +1243,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     case 6: e = launch_cm<6>(pl, fa, s); break;
     default: e = launch_cm<8>(pl, fa, s); break;
   }
-  else switch (pl.dim_pad) {
-    case 2: e = launch_ns<2>(pl, fa, s); break;
-    case 4: e = launch_ns<4>(pl, fa, s); break;
-    case 6: e = launch_ns<6>(pl, fa, s); break;
-    default: e = launch_ns<8>(pl, fa, s); break;
-  }
+  else return BO_ERR_UNSUPPORTED;
   if (e != hipSuccess) return BO_ERR_HIP;
   if (timed) timer_mark(s);
   if (d->topq > 0) {
