@@ -138,10 +138,10 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     [n_obj, N, N] (invert_k output) -- device f64 tensors or arrays.  Returns a dict with
     the requested outputs (device tensors [n_obj, count] / [count]) and, if topq > 0,
     ``top_val`` / ``top_idx`` (device [topq]; index -1 = no candidate).  Asynchronous
-    on the current stream.  mode "auto" lets the library use the triangular variance
-    formulation q = |R^T k|^2 with K^-1 = R R^T (N <= 512, half the matrix-core work; falls
-    back to dense on the device if K^-1 is not numerically positive definite); "dense" is
-    update_variance's k^T (K^-1 k) verbatim.  The "-exp" modes disable the integer-grid
+    on the current stream.  mode "auto" computes the variance's quadratic form as
+    q = 2 k^T (U k), U = upper triangle of (K^-1 + K^-T)/2 with the diagonal halved (the same
+    form, half the matrix-core work, no factorisation); "dense" is update_variance's
+    k^T (K^-1 k) verbatim.  The "-exp" modes disable the integer-grid
     separable K* generation (exp table) and evaluate every K* entry with exp().
     """
     dev = require_device(device)

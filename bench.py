@@ -55,7 +55,7 @@ def flops_per_candidate(n=N_TRAIN, n_obj=N_OBJ, d=DIM):
 def executed_mfma_flops_per_candidate(mode, n=N_TRAIN, n_obj=N_OBJ):
     """Matrix-core flops the fused kernel actually issues per candidate (16x16x4 f64 MFMA,
     2048 flops, 16 candidates per wave): dense walks all (NS/8) E-pairs x (NS/2) k-step pairs,
-    triangular only the upper chunks c >= ep."""
+    upper only the blocks ep <= c (q = 2 k.(U k), U = upper triangle of sym(K^-1))."""
     ns = -(-n // 4)
     ns = next(v for v in (8, 16, 32, 64, 96, 128) if v >= ns) if n <= 512 else ns
     pairs = ns * ns // 16 if mode == "dense" else ns * ns // 32 + ns // 4
@@ -132,7 +132,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("auto", "dense"), default="auto",
-                    help="variance formulation (auto = triangular |R^T k|^2 when N <= 512)")
+                    help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved)")
     args = ap.parse_args()
 
     import torch
@@ -224,9 +224,10 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F64_MATRIX_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_F64_MATRIX_TFLOPS,
                          "traffic": pmc_traffic(),
-                         "kernel": "fused_predict_kernel<128,2,false,false>",
+                         "kernel": ("cm_predict_kernel<2, true, true>" if args.mode == "auto"
+                                    else "cm_predict_kernel<2, true, false>"),
                          "kernel_ms": k_ms, "flops_per_candidate": f,
-                         "formulation": ("triangular: K^-1 = R R^T, q = |R^T k|^2" if args.mode == "auto"
+                         "formulation": ("upper: q = 2 k.(U k), U = triu((K^-1 + K^-T)/2), diag/2" if args.mode == "auto"
                                          else "dense: q = k^T (K^-1 k)"),
                          "executed_mfma_flops_per_candidate": fx,
                          "executed_mfma_tflops": fx * per_rank / (k_ms * 1e-3) / 1e12,

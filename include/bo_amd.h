@@ -64,10 +64,10 @@ int bo_device_count(void);
  * against K^-1 on the f64 matrix cores and reduced to outputs in one pass.
  * ---------------------------------------------------------------------------------- */
 /* Variance formulation.  DENSE: q = k^T (K^-1 k) exactly as update_variance (2N^2 flops per
- * candidate and objective).  AUTO: when N <= 512 the library factors the given K^-1 = R R^T
- * (Cholesky, on the device) and computes q = |R^T k|^2 (N^2 flops: half the matrix-core
- * work); if that factorisation fails (K^-1 not numerically positive definite) it falls back
- * to DENSE on the device, without a host round trip. */
+ * candidate and objective).  AUTO (default): q = 2 k^T (U k) with U the upper triangle of
+ * sym(K^-1) = (K^-1 + K^-T)/2 and its diagonal halved -- the same quadratic form (k^T A k =
+ * k^T sym(A) k), half the matrix-core work, no factorisation and no positive-definiteness
+ * requirement. */
 /* mode is a bit set: BO_PREDICT_DENSE forces the dense formulation; BO_PREDICT_NO_SEPARABLE
  * disables the integer-grid fast K* generation (K* = pv * R(f) * T[x_last - c_last], an exp
  * table over the last grid axis; used only when the candidates are a grid whose last axis is
