@@ -18,8 +18,8 @@ resident in HBM before the timed region.
 
 Prints ONE JSON line (rank 0).  `roofline` is the fused kernel's f64 matrix-core throughput
 (algorithmic flops F per candidate, SURVEY.md §8d) over its HIP-event-timed launches;
-`cpu_baseline` times the CPU oracle (oracle/oracle_np.py, the reference algorithm) on a
-bounded slice of the same workload on this host.
+`cpu_baseline` times the C/OpenMP restatement of the reference algorithm (oracle/cpu_ref.c)
+on a bounded slice of the same workload on this host's cores.
 """
 
 from __future__ import annotations
@@ -84,31 +84,42 @@ def make_problem(world):
     return x, y, pm, pv, ls, betas, kinv, rows
 
 
-def cpu_baseline(x, y, pm, pv, ls, betas, kinv, budget_s=12.0, chunk=8192, max_cand=131072):
-    """Reference algorithm on the host (oracle/oracle_np.py): materialised k_star chunk,
-    BLAS dgemm K^-1 K*, quadratic form, standardise, UCB, Sigma-UCB; then argsort select."""
-    from oracle import oracle_np as O
+def _cpu_model():
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
-    except Exception:  # pragma: no cover
-        cores = os.cpu_count() or 1
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(x, y, pm, pv, ls, betas, kinv, budget_s=12.0, chunk=16384, max_cand=SIDE * SIDE):
+    """Reference algorithm on the host cores: oracle/cpu_ref.c, the C/OpenMP restatement of
+    update_k_star -> update_mean -> update_variance (materialised K* per candidate block,
+    DGEMM K^-1 K*, the serial quadratic form) -> standardise -> UCB -> Sigma-UCB, then
+    select_next_batch's full descending sort + exclusion walk."""
+    from oracle import cpu_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cpu_ref.load()
     done = 0
-    t0 = time.perf_counter()
     acqs = []
+    t0 = time.perf_counter()
     while done < max_cand and time.perf_counter() - t0 < budget_s:
         lin = np.arange(done, done + chunk)
-        pts = np.stack([lin // SIDE, lin % SIDE], axis=1).astype(np.int64)
-        r = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv, chunk=chunk)
-        acqs.append(r["acq"])
+        pts = np.stack([lin // SIDE, lin % SIDE], axis=1).astype(np.float64)
+        acqs.append(cpu_ref.predict_acquire(x, y, pts, kinv, pm, pv, ls, betas, threads=threads,
+                                            outputs=True)["acq"])
         done += chunk
-    acq = np.concatenate(acqs)
-    np.argsort(acq)[::-1]
+    lin = np.arange(done)
+    cpu_ref.select(np.concatenate(acqs), np.stack([lin // SIDE, lin % SIDE], axis=1).astype(np.float64),
+                   x, TOPQ)
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "candidate-points/sec", "cores": int(cores), "kind": "port",
-            "sample": f"first {done} candidates of the C3 grid (N_train=512, 2 objectives), "
-                      f"oracle/oracle_np.py restatement: chunked k_star + BLAS dgemm + argsort, "
-                      f"{dt:.1f} s"}
+    return {"value": done / dt, "unit": "candidate-points/sec", "cores": threads, "kind": "port",
+            "sample": f"first {done} candidates of the C3 grid (N_train=512, 2 objectives, mu/var/acq "
+                      f"written, top-{TOPQ} select), oracle/cpu_ref.c (C/OpenMP, {threads} threads of "
+                      f"{os.cpu_count()} logical CPUs, {_cpu_model()}), {dt:.1f} s"}
 
 
 def pmc_traffic():

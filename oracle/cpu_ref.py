@@ -1,0 +1,78 @@
+"""ctypes binding of oracle/cpu_ref.c (the C/OpenMP restatement of the reference chain).
+
+TEST / MEASUREMENT INFRASTRUCTURE ONLY: used by tests/ (pinned against oracle_np) and by
+bench.py's cpu_baseline leg; never by bayesopt_smart_amd.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "cpu_ref.c")
+LIB = os.path.join(HERE, "libcpu_ref.so")
+# portable x86-64 (AVX2 + FMA): the GPU box's host CPU is not this container's
+FLAGS = ["-O3", "-march=x86-64-v3", "-fopenmp", "-shared", "-fPIC"]
+
+_lib = None
+
+
+def build():
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        subprocess.run(["gcc", *FLAGS, SRC, "-o", LIB, "-lm"], check=True)
+    return LIB
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = C.CDLL(LIB)
+        P = C.c_void_p
+        lib.bo_cpu_predict_acquire.argtypes = [C.c_int, C.c_int, C.c_int, P, P, P, C.c_long, P, P, P,
+                                               P, P, P, P, P, C.c_int]
+        lib.bo_cpu_predict_acquire.restype = C.c_int
+        lib.bo_cpu_select.argtypes = [P, P, C.c_long, C.c_int, P, C.c_long, C.c_int, P]
+        lib.bo_cpu_select.restype = C.c_int
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def predict_acquire(x, y, cand, kinv, pm, pv, ls, betas, threads=None, outputs=True):
+    """mu, var (optional) and acq over `cand` (f64 [M, d]) with the reference's algorithm."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    n, d = x.shape
+    n_obj = len(pm)
+    y = np.ascontiguousarray(np.asarray(y, dtype=np.float64)[:n, :n_obj])
+    cand = np.ascontiguousarray(cand, dtype=np.float64)
+    m = cand.shape[0]
+    kinv = np.ascontiguousarray(np.asarray(kinv, dtype=np.float64)[:, :n, :n])
+    vec = lambda v: np.ascontiguousarray(np.asarray(v, dtype=np.float64)[:n_obj])  # noqa: E731
+    mu = np.empty((n_obj, m)) if outputs else None
+    var = np.empty((n_obj, m)) if outputs else None
+    acq = np.empty(m)
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    load().bo_cpu_predict_acquire(n, d, n_obj, _p(x), _p(y), _p(cand), m, _p(kinv), _p(vec(pm)),
+                                  _p(vec(pv)), _p(vec(ls)), _p(vec(betas)), _p(mu), _p(var), _p(acq),
+                                  threads)
+    return {"mu": mu, "var": var, "acq": acq}
+
+
+def select(acq, cand, excl, q):
+    """Candidate indices of select_next_batch's choice (descending, evaluated points skipped)."""
+    acq = np.ascontiguousarray(acq, dtype=np.float64)
+    cand = np.ascontiguousarray(cand, dtype=np.float64)
+    excl = np.ascontiguousarray(excl, dtype=np.float64).reshape(-1, cand.shape[1])
+    out = np.empty(q, dtype=np.int64)
+    load().bo_cpu_select(_p(acq), _p(cand), cand.shape[0], cand.shape[1], _p(excl), excl.shape[0], q,
+                         _p(out))
+    return out

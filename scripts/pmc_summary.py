@@ -1,0 +1,52 @@
+"""Summarise the rocprofv3 PMC passes of scripts/pmc.sh for the fused C3 kernel.
+
+    python scripts/pmc_summary.py gpurun_out/pmc profiles/r01_c3_pmc.json
+
+Per-launch means over the cm_predict_kernel dispatches of each pass.  HBM bytes follow the
+MI355X guide's HBM/rocprofv3 section: FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
+reports half the bytes of 16-B-per-lane streaming reads (the packed W stream is exactly that),
+so it is doubled; WRITE_SIZE is exact for the 16-B stores of the epilogue.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNEL = "cm_predict_kernel"
+
+
+def main(src, dst):
+    vals = defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(src, "p*", "*counter_collection.csv"))):
+        with open(f) as fh:
+            per_dispatch = defaultdict(dict)
+            for row in csv.DictReader(fh):
+                if KERNEL not in row["Kernel_Name"]:
+                    continue
+                d = per_dispatch[row["Dispatch_Id"]]
+                d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+            for d in per_dispatch.values():
+                for k, v in d.items():
+                    vals[k].append(v)
+    mean = {k: sum(v) / len(v) for k, v in vals.items()}
+    out = {"workload": "C3", "kernel": "cm_predict_kernel<2, true, true>",
+           "counters_per_launch": mean, "launches_per_counter": {k: len(v) for k, v in vals.items()}}
+    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+        fetch = 2.0 * mean["FETCH_SIZE"] * 1024.0       # gfx950 16-B-read correction
+        write = mean["WRITE_SIZE"] * 1024.0
+        out.update({"fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+                    "hbm_bytes_per_launch": fetch + write,
+                    "algorithmic_bytes_per_launch": 40 * 1048576,
+                    "note": "FETCH_SIZE x2 (gfx950 16-B streaming-read correction), KiB -> B; "
+                            "algorithmic = 40 B/candidate (mu, var, acq f64 written; grid generated)"})
+    if "SQ_INSTS_MFMA" in mean and "SQ_INSTS_VALU" in mean:
+        out["valu_per_mfma"] = mean["SQ_INSTS_VALU"] / max(mean["SQ_INSTS_MFMA"], 1.0)
+    with open(dst, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -94,3 +94,19 @@ def test_select_indices_matches_reference_walk(golden):
     excl = np.array([np.any(np.all(c == x, axis=1)) for c in cand])
     idx = O.select_next_batch_indices(acq, excl, 16)
     np.testing.assert_array_equal(cand[idx], d["select_q16"])
+
+
+@pytest.mark.parametrize("name", ["g1_predict_2d", "g2_predict_512", "g3_predict_6d3o"])
+def test_cpu_ref_matches_oracle(golden, name):
+    """oracle/cpu_ref.c (bench.py's timed CPU baseline) against the reference's own outputs."""
+    from oracle import cpu_ref
+    d = golden(name)
+    kinv = kinv_of(d)
+    out = cpu_ref.predict_acquire(d["x"], d["y"], d["cand"], kinv, d["pm"], d["pv"], d["ls"],
+                                  d["betas"], threads=4)
+    from parity import check_predict
+    check_predict({k: out[k] for k in ("mu", "var", "acq")}, d, d["pv"])
+    # the selection itself, with the reference's own acq values as input, is exact
+    for q in (3, 16):
+        sel = cpu_ref.select(d["acq"], d["cand"], d["x"], q)
+        np.testing.assert_array_equal(d["cand"][sel], d[f"select_q{q}"])
