@@ -36,15 +36,24 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-N_TRAIN = 512
-SIDE = 1024
-N_OBJ = 2
-DIM = 2
-TOPQ = 3
-LS = 20.0
-BETA = 2.0
 PEAK_F64_MATRIX_TFLOPS = 78.6        # MI355X dense FP64 matrix peak (datasheet)
 PEAK_HBM_GBPS = 8000.0
+
+# BASELINE.json configs (SURVEY.md §8 table / §8d synthetic inputs).  C3 is the headline
+# (the default); C2 / C4 / C5 are selectable with --config for their own timings.
+CONFIGS = {
+    "C2": dict(dim=2, n_obj=2, n_train=128, side=512, ls=20.0, q=3, kind="grid", scaling="weak",
+               workload="C2: 2D/2-obj toy_function, N_train=128, N_cand=262,144 per GPU ('ij' grid), UCB + Sigma-UCB, q=3"),
+    "C3": dict(dim=2, n_obj=2, n_train=512, side=1024, ls=20.0, q=3, kind="grid", scaling="weak",
+               workload="C3: 2D/2-obj toy_function, N_train=512, N_cand=1,048,576 per GPU ('ij' integer grid), HVI (Sigma-UCB), q=3"),
+    "C4": dict(dim=6, n_obj=3, n_train=1024, m=1 << 21, ls=40.0, q=3, kind="sobol", scaling="strong",
+               workload="C4: 6D/3-obj toy_function_3d, N_train=1024, N_cand=2,097,152 unscrambled Sobol in [0,300)^6 sharded over the GPUs, HVI (Sigma-UCB), q=3"),
+    "C5": dict(dim=6, n_obj=3, n_train=2048, m=1 << 22, ls=40.0, q=16, kind="sobol", scaling="strong",
+               workload="C5: 6D/3-obj toy_function_3d, N_train=2048, N_cand=4,194,304 unscrambled Sobol in [0,300)^6 sharded over the GPUs, HVI (Sigma-UCB), q=16"),
+}
+BETA = 2.0
+# C3 constants (cpu_baseline's sample is the C3 grid)
+N_TRAIN, SIDE, N_OBJ, DIM, TOPQ = 512, 1024, 2, 2, 3
 
 
 def flops_per_candidate(n=N_TRAIN, n_obj=N_OBJ, d=DIM):
@@ -53,13 +62,13 @@ def flops_per_candidate(n=N_TRAIN, n_obj=N_OBJ, d=DIM):
 
 
 def executed_mfma_flops_per_candidate(mode, n=N_TRAIN, n_obj=N_OBJ):
-    """Matrix-core flops the fused kernel actually issues per candidate (16x16x4 f64 MFMA,
-    2048 flops, 16 candidates per wave): dense walks all (NS/8) E-pairs x (NS/2) k-step pairs,
-    upper only the blocks ep <= c (q = 2 k.(U k), U = upper triangle of sym(K^-1))."""
-    ns = -(-n // 4)
-    ns = next(v for v in (8, 16, 32, 64, 96, 128) if v >= ns) if n <= 512 else ns
-    pairs = ns * ns // 16 if mode == "dense" else ns * ns // 32 + ns // 4
-    return n_obj * pairs * 4 * 2048 // 16
+    """Matrix-core flops the chunk-major kernel issues per candidate (16x16x4 f64 MFMA = 2048
+    flops, 16 candidates per wave, nch = padded N / 32 chunks of 32 rows): dense issues
+    16 nch^2 MFMAs per 16 candidates and objective, upper the blocks ep <= c only,
+    8 nch (nch + 1) (q = 2 k.(U k), U = upper triangle of sym(K^-1))."""
+    nch = -(-n // 32)
+    mfmas = 16 * nch * nch if mode == "dense" else 8 * nch * (nch + 1)
+    return n_obj * mfmas * 2048 // 16
 
 
 def toy_function(x):
@@ -67,21 +76,48 @@ def toy_function(x):
     return np.stack([-((x[:, 0] - 150) ** 2) + 100, -((x[:, 1] - 150) ** 2) + 20], axis=1)
 
 
-def make_problem(world):
-    rng = np.random.default_rng(0)
-    rows = SIDE * world
-    lin = rng.choice(rows * SIDE, size=N_TRAIN, replace=False)
-    x = np.stack([lin // SIDE, lin % SIDE], axis=1).astype(np.float64)
-    y = toy_function(x)
-    pm, pv = y.mean(0), y.var(0)                               # compute_prior_mean / _variance
-    ls = np.full(N_OBJ, LS)
-    betas = np.full(N_OBJ, BETA)
-    # K + 1e-6 I and its inverse (update_k / invert_k, numba_kernels.py:329-403): setup only
+def toy_function_3d(x):
+    """examples/benchmark_functions.py:58-73 (3 objectives from x[0..2])."""
+    return np.stack([-((x[:, 0] - 150) ** 2) + 100, -((x[:, 1] - 150) ** 2) + 20,
+                     -((x[:, 2] - 5) ** 2) + 120], axis=1)
+
+
+def _kinv(x, pv, ls):
+    """K + 1e-6 I and its inverse (update_k / invert_k, numba_kernels.py:329-403): setup only."""
     diff = x[:, None, :] - x[None, :, :]
     sq = np.einsum("ijd,ijd->ij", diff, diff)
-    kinv = np.stack([np.linalg.inv(pv[o] * np.exp(-0.5 * sq / ls[o] ** 2) + 1e-6 * np.eye(N_TRAIN))
-                     for o in range(N_OBJ)])
-    return x, y, pm, pv, ls, betas, kinv, rows
+    n = x.shape[0]
+    return np.stack([np.linalg.inv(pv[o] * np.exp(-0.5 * sq / ls[o] ** 2) + 1e-6 * np.eye(n))
+                     for o in range(len(pv))])
+
+
+def make_config_problem(cfg, world):
+    """Seeded inputs of SURVEY.md §8d.  Returns (x, y, pm, pv, ls, betas, kinv, cand) where cand
+    is ('grid', rows, side) or ('sobol', points [M, d] f64)."""
+    rng = np.random.default_rng(0)
+    if cfg["kind"] == "grid":
+        side = cfg["side"]
+        rows = side * world
+        lin = rng.choice(rows * side, size=cfg["n_train"], replace=False)
+        x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+        y = toy_function(x)
+        cand = ("grid", rows, side)
+    else:
+        from scipy.stats import qmc
+        pts = qmc.Sobol(cfg["dim"], scramble=False).random(cfg["m"]) * 300.0
+        x = pts[rng.choice(cfg["m"], size=cfg["n_train"], replace=False)]
+        y = toy_function_3d(x)
+        cand = ("sobol", pts)
+    pm, pv = y.mean(0), y.var(0)                               # compute_prior_mean / _variance
+    ls = np.full(cfg["n_obj"], cfg["ls"])
+    betas = np.full(cfg["n_obj"], BETA)
+    return x, y, pm, pv, ls, betas, _kinv(x, pv, ls), cand
+
+
+def make_problem(world):
+    """C3 problem (scripts/ablate.py, tests): (x, y, pm, pv, ls, betas, kinv, grid rows)."""
+    x, y, pm, pv, ls, betas, kinv, cand = make_config_problem(CONFIGS["C3"], world)
+    return x, y, pm, pv, ls, betas, kinv, cand[1]
 
 
 def _cpu_model():
@@ -95,11 +131,13 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(x, y, pm, pv, ls, betas, kinv, budget_s=12.0, chunk=16384, max_cand=SIDE * SIDE):
+def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, budget_s=12.0, chunk=16384,
+                 max_cand=SIDE * SIDE):
     """Reference algorithm on the host cores: oracle/cpu_ref.c, the C/OpenMP restatement of
     update_k_star -> update_mean -> update_variance (materialised K* per candidate block,
     DGEMM K^-1 K*, the serial quadratic form) -> standardise -> UCB -> Sigma-UCB, then
-    select_next_batch's full descending sort + exclusion walk."""
+    select_next_batch's full descending sort + exclusion walk.
+    points(lo, hi) -> f64 [hi - lo, d] candidates of the workload."""
     from oracle import cpu_ref
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     cpu_ref.load()
@@ -107,19 +145,15 @@ def cpu_baseline(x, y, pm, pv, ls, betas, kinv, budget_s=12.0, chunk=16384, max_
     acqs = []
     t0 = time.perf_counter()
     while done < max_cand and time.perf_counter() - t0 < budget_s:
-        lin = np.arange(done, done + chunk)
-        pts = np.stack([lin // SIDE, lin % SIDE], axis=1).astype(np.float64)
-        acqs.append(cpu_ref.predict_acquire(x, y, pts, kinv, pm, pv, ls, betas, threads=threads,
-                                            outputs=True)["acq"])
+        acqs.append(cpu_ref.predict_acquire(x, y, points(done, done + chunk), kinv, pm, pv, ls, betas,
+                                            threads=threads, outputs=True)["acq"])
         done += chunk
-    lin = np.arange(done)
-    cpu_ref.select(np.concatenate(acqs), np.stack([lin // SIDE, lin % SIDE], axis=1).astype(np.float64),
-                   x, TOPQ)
+    cpu_ref.select(np.concatenate(acqs), points(0, done), x, q)
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "candidate-points/sec", "cores": threads, "kind": "port",
-            "sample": f"first {done} candidates of the C3 grid (N_train=512, 2 objectives, mu/var/acq "
-                      f"written, top-{TOPQ} select), oracle/cpu_ref.c (C/OpenMP, {threads} threads of "
-                      f"{os.cpu_count()} logical CPUs, {_cpu_model()}), {dt:.1f} s"}
+            "sample": f"first {done} candidates of the {label} (N_train={x.shape[0]}, {len(pm)} "
+                      f"objectives, mu/var/acq written, top-{q} select), oracle/cpu_ref.c (C/OpenMP, "
+                      f"{threads} threads of {os.cpu_count()} logical CPUs, {_cpu_model()}), {dt:.1f} s"}
 
 
 def pmc_traffic():
@@ -141,10 +175,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="C3",
+                    help="BASELINE.json config (C3 = the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("auto", "dense"), default="auto",
                     help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved)")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
 
     import torch
     import torch.distributed as dist
@@ -162,22 +199,32 @@ def main():
     import bayesopt_smart_amd as bo
     lib = bo._lib.load()
 
-    x, y, pm, pv, ls, betas, kinv, rows = make_problem(world)
-    cands = bo.CandidateSet.grid([(0, rows), (0, SIDE)])
-    per_rank = SIDE * SIDE
-    offset = rank * per_rank
+    x, y, pm, pv, ls, betas, kinv, cand = make_config_problem(cfg, world)
+    n_obj, q = cfg["n_obj"], cfg["q"]
+    if cand[0] == "grid":
+        # weak scaling: rank r owns grid rows [side r, side (r + 1)) of a (side P) x side grid
+        side = cand[2]
+        cands = bo.CandidateSet.grid([(0, cand[1]), (0, side)])
+        per_rank = side * side
+        offset = rank * per_rank
+    else:
+        # strong scaling: the fixed Sobol set split into P contiguous index ranges
+        m = cand[1].shape[0]
+        per_rank = m // world
+        offset = rank * per_rank
+        cands = bo.CandidateSet.explicit(cand[1], device=dev)
     xd = torch.tensor(x, device=dev)
     yd = torch.tensor(y, device=dev)
     kd = torch.tensor(kinv, device=dev)
-    out = {"mu": torch.empty((N_OBJ, per_rank), dtype=torch.float64, device=dev),
-           "var": torch.empty((N_OBJ, per_rank), dtype=torch.float64, device=dev),
-           "acq": torch.empty(per_rank, dtype=torch.float64, device=dev)}
-    gath_v = torch.empty(world * TOPQ, dtype=torch.float64, device=dev)
-    gath_i = torch.empty(world * TOPQ, dtype=torch.int64, device=dev)
+    outputs = ("mu", "var", "ucb", "acq") if args.config == "C2" else ("mu", "var", "acq")
+    out = {k: torch.empty((per_rank,) if k == "acq" else (n_obj, per_rank), dtype=torch.float64,
+                          device=dev) for k in outputs}
+    gath_v = torch.empty(world * q, dtype=torch.float64, device=dev)
+    gath_i = torch.empty(world * q, dtype=torch.int64, device=dev)
 
     def step():
-        r = bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=("mu", "var", "acq"),
-                               topq=TOPQ, offset=offset, count=per_rank, out=out, device=dev,
+        r = bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=outputs,
+                               topq=q, offset=offset, count=per_rank, out=out, device=dev,
                                mode=args.mode)
         if world > 1:
             dist.all_gather_into_tensor(gath_v, r["top_val"])
@@ -185,7 +232,7 @@ def main():
             v, i = gath_v.cpu().numpy(), gath_i.cpu().numpy()
         else:
             v, i = r["top_val"].cpu().numpy(), r["top_idx"].cpu().numpy()
-        return bo.merge_topq(v, i, TOPQ)
+        return bo.merge_topq(v, i, q)
 
     for _ in range(args.warmup):
         step()
@@ -212,31 +259,35 @@ def main():
         k_ms = kms.value / max(nl.value, 1)
 
     if rank == 0:
-        f = flops_per_candidate()
-        fx = executed_mfma_flops_per_candidate(args.mode)
+        n, d = cfg["n_train"], cfg["dim"]
+        f = flops_per_candidate(n, n_obj, d)
+        fx = executed_mfma_flops_per_candidate(args.mode, n, n_obj)
         achieved = f * per_rank / (k_ms * 1e-3) / 1e12
+        total = world * per_rank
+        metric = ("candidate-points/sec (GP predict + HVI) at N_train=512, N_cand=1M" if args.config == "C3"
+                  else f"candidate-points/sec (GP predict + HVI), BASELINE config {args.config}")
         res = {
-            "metric": "candidate-points/sec (GP predict + HVI) at N_train=512, N_cand=1M",
-            "value": world * per_rank / t_step,
+            "metric": metric,
+            "value": total / t_step,
             "unit": "candidate-points/sec",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": t_step * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": cfg["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (toy_function on a seeded 512-point design)",
-            "config": {"workload": "C3: 2D/2-obj toy_function, N_train=512, N_cand=1,048,576 per GPU "
-                                   "('ij' integer grid), HVI (Sigma-UCB), q=3",
-                       "n_train": N_TRAIN, "n_cand_per_gpu": per_rank, "n_objectives": N_OBJ,
-                       "dim": DIM, "topq": TOPQ, "parallelism": f"candidate-shard x{world}"},
+            "data": ("synthetic (toy_function on a seeded design)" if cand[0] == "grid" else
+                     "synthetic (toy_function_3d on a seeded design drawn from the Sobol set)"),
+            "config": {"workload": cfg["workload"], "n_train": n, "n_cand_per_gpu": per_rank,
+                       "n_cand_total": total, "n_objectives": n_obj, "dim": d, "topq": q,
+                       "parallelism": f"candidate-shard x{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F64_MATRIX_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_F64_MATRIX_TFLOPS,
-                         "traffic": pmc_traffic(),
-                         "kernel": ("cm_predict_kernel<2, true, true>" if args.mode == "auto"
-                                    else "cm_predict_kernel<2, true, false>"),
+                         "traffic": pmc_traffic() if args.config == "C3" else None,
+                         "kernel": (f"cm_predict_kernel<{2 if d <= 2 else 6}, {'true' if cand[0] == 'grid' else 'false'}, "
+                                    f"{'true' if args.mode == 'auto' else 'false'}>"),
                          "kernel_ms": k_ms, "flops_per_candidate": f,
                          "formulation": ("upper: q = 2 k.(U k), U = triu((K^-1 + K^-T)/2), diag/2" if args.mode == "auto"
                                          else "dense: q = k^T (K^-1 k)"),
@@ -246,7 +297,19 @@ def main():
             "selected": [int(i) for i in sel[1]],
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(x, y, pm, pv, ls, betas, kinv)
+            if cand[0] == "grid":
+                side = cand[2]
+
+                def points(lo, hi):
+                    lin = np.arange(lo, hi)
+                    return np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+                label = f"{args.config} grid"
+            else:
+                def points(lo, hi):
+                    return cand[1][lo:hi]
+                label = f"{args.config} Sobol set"
+            res["cpu_baseline"] = cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q,
+                                               max_cand=per_rank)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
