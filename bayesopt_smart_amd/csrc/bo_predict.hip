@@ -28,6 +28,7 @@
 #include <string.h>
 #include <math.h>
 
+#include <type_traits>
 #include <vector>
 
 #ifdef BO_ABL_STAMPS
@@ -489,6 +490,24 @@ __global__ __launch_bounds__(256, 1) void fused_predict_kernel(const FusedArgs a
 // ---------------------------------------------------------------------------------------
 constexpr int kCMaxEp = 16;              // E-pairs (32 rows each): N <= 512
 
+// Nested guards over the unrolled E-pair bodies: body E runs iff E < n, and is entered only
+// from body E - 1 (see chunk_step in cm_tiles).
+template <int E, int N>
+struct EpChain {
+  template <class F>
+  static __device__ __forceinline__ void run(F& f, int n) {
+    if (E < n) {
+      f(std::integral_constant<int, E>{});
+      EpChain<E + 1, N>::run(f, n);
+    }
+  }
+};
+template <int N>
+struct EpChain<N, N> {
+  template <class F>
+  static __device__ __forceinline__ void run(F&, int) {}
+};
+
 template <int DIM, bool SEP>
 struct KRows {
   const double* rv;   // SEP: [n_pad] pv * R(f) (0 for padded rows)
@@ -628,29 +647,32 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #pragma unroll
             for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * ch + 4 * s + g], B[s], mpart);
           }
-          // the group's E-pairs touching chunk ch, ascending: e0 + e <= ch (upper) or all (a
-          // prefix of the unrolled sequence either way, which keeps hipcc's vmcnt waits exact)
+          // the group's E-pairs touching chunk ch, ascending: the first n_here of them (e0 + e
+          // <= ch when upper).  EpChain nests the guards (body e+1 is reached only from body e),
+          // so every body has one predecessor and hipcc's vmcnt waits inside the chunk stay
+          // exact; independent guards made every body a join and cost a vmcnt(0) drain of the
+          // W ring per E-pair.
+          const int n_here = upper ? (ch - e0 + 1 < eN ? ch - e0 + 1 : eN) : eN;
+          auto ep_body = [&](auto e_c) {
+            constexpr int e = decltype(e_c)::value;
 #pragma unroll
-          for (int e = 0; e < kCMaxEp; ++e) {
-            if (e < eN && (!upper || e0 + e <= ch)) {
-#pragma unroll
-              for (int pp = 0; pp < 4; ++pp) {
-                // MFMAs first, then the refill of the same ring slot (no operand copies)
-                acc[e][0] = mfma64(wa[pp].x, B[2 * pp], acc[e][0]);
-                acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
-                acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
-                acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
-                const int so = base + ((pos + kPF) << 11);
+            for (int pp = 0; pp < 4; ++pp) {
+              // MFMAs first, then the refill of the same ring slot (no operand copies)
+              acc[e][0] = mfma64(wa[pp].x, B[2 * pp], acc[e][0]);
+              acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
+              acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
+              acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
+              const int so = base + ((pos + kPF) << 11);
 #ifndef BO_ABL_NOLOAD
-                wa[pp] = wload(wr, voff, so);
-                wb[pp] = wload(wr, voff, so + 1024);
+              wa[pp] = wload(wr, voff, so);
+              wb[pp] = wload(wr, voff, so + 1024);
 #else   // ablation build only: no W stream (operands stay in the ring)
-                asm volatile("" : "+v"(wa[pp]), "+v"(wb[pp]) : "s"(so));
+              asm volatile("" : "+v"(wa[pp]), "+v"(wb[pp]) : "s"(so));
 #endif
-                ++pos;
-              }
+              ++pos;
             }
-          }
+          };
+          EpChain<0, kCMaxEp>::run(ep_body, n_here);
         };
         const int c0 = upper ? e0 : 0;
         double BX[8], BY[8];
