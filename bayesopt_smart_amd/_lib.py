@@ -77,6 +77,10 @@ _SIGS = {
                                  C.c_int32, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
     "bo_select_topq_workspace_size": (C.c_size_t, [C.c_int64, C.c_int32]),
     "bo_pareto_mask": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, c_vp]),
+    "bo_hvi_boxes": (C.c_int, [c_dbl_p, C.c_int64, C.c_int32, c_dbl_p, c_vp, C.c_int64,
+                               C.POINTER(C.c_int64)]),
+    "bo_hypervolume_improvement_exact": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int64, C.c_int32,
+                                                   c_dbl_p, c_dbl_p, c_vp, C.c_int64, c_vp]),
     "bo_invert_k": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, C.c_size_t, c_vp]),
     "bo_invert_k_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
     "bo_compute_mll": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,

@@ -97,3 +97,66 @@ def select_next_batch(input_space, acquisition_values, evaluated_points, batch_s
         return input_space[torch.as_tensor(idx, device=input_space.device)].cpu().numpy()
     return np.asarray(input_space)[idx]
 
+
+
+# ------------------------------------------------------- exact hypervolume improvement
+def hypervolume_boxes(front, reference_point) -> np.ndarray:
+    """Disjoint boxes [lower, upper) (rows of 2*n_obj, upper may be +inf) covering the region
+    above `reference_point` that no row of `front` dominates (maximisation); host decomposition
+    in the library (bo_hvi_boxes).  Not in the reference (its reference point is unused,
+    bayesian_optimization.py:65)."""
+    f = np.ascontiguousarray(np.asarray(front.cpu().numpy() if isinstance(front, torch.Tensor) else front,
+                                        dtype=np.float64))
+    r = np.ascontiguousarray(np.asarray(reference_point, dtype=np.float64).ravel())
+    n_obj = r.size
+    f = f.reshape(-1, n_obj)
+    lib = _lib.load()
+    cnt = C_i64(0)
+    dp = _C.POINTER(_C.c_double)
+    cap = 1024
+    while True:
+        out = np.empty((cap, 2 * n_obj), dtype=np.float64)
+        st = lib.bo_hvi_boxes(f.ctypes.data_as(dp), f.shape[0], n_obj, r.ctypes.data_as(dp),
+                              out.ctypes.data, cap, _C.byref(cnt))
+        if st == 3 and cnt.value > cap:      # BO_ERR_WORKSPACE: retry with the reported count
+            cap = int(cnt.value)
+            continue
+        _lib.check(st, "bo_hvi_boxes")
+        return out[: cnt.value].copy()
+
+
+def hypervolume_improvement_exact(ucb, front, reference_point, prior_mean, prior_variance, out=None):
+    """Exact HVI of every candidate's UCB vector over `front`: acq = HV(front u {u}) - HV(front),
+    u_k = prior_mean_k + sqrt(prior_variance_k) * ucb[k] (ucb: the reference's standardised
+    per-objective UCB array, [n_obj, M], numpy or HIP tensor).  Returns acq ([M], a device
+    tensor, or numpy for numpy `ucb`); written into `out` when given (in place)."""
+    dev = _dev_of(out, ucb)
+    u = _Arg(ucb, dev)
+    n_obj, n = u.t.shape
+    boxes = torch.as_tensor(hypervolume_boxes(front, reference_point), device=dev)
+    acq = _Arg(out, dev, write=True) if out is not None else None
+    dst = acq.t if acq is not None else torch.empty(n, dtype=F64, device=dev)
+    pm = np.asarray(prior_mean, dtype=np.float64)[:n_obj]
+    sc = np.sqrt(np.asarray(prior_variance, dtype=np.float64)[:n_obj])
+    _lib.check(_lib.load().bo_hypervolume_improvement_exact(
+        dst.data_ptr(), u.ptr, u.t.stride(0), n, n_obj, _host_vec(pm, n_obj), _host_vec(sc, n_obj),
+        boxes.data_ptr() if boxes.numel() else None, boxes.shape[0], stream_handle(dev)),
+        "bo_hypervolume_improvement_exact")
+    if acq is not None:
+        acq.finish()
+        return out
+    return dst if isinstance(ucb, torch.Tensor) else dst.cpu().numpy()
+
+
+def update_hypervolume_improvement_exact(acquisition_values, ucb, y_vector, n_evaluations,
+                                         reference_point, prior_mean, prior_variance):
+    """The acquisition update of the loop (bayesian_optimization.py:195-199) as an exact HVI:
+    the front is the Pareto-efficient subset (device filter, pareto.py:12-45) of the evaluated
+    objectives y_vector[:n_evaluations]; in place into `acquisition_values`."""
+    from .pareto import is_pareto_efficient
+    y = y_vector[:n_evaluations]
+    front = y[is_pareto_efficient(y)] if n_evaluations > 0 else np.zeros((0, len(reference_point)))
+    if isinstance(front, torch.Tensor):
+        front = front.cpu().numpy()
+    hypervolume_improvement_exact(ucb, front, reference_point, prior_mean, prior_variance,
+                                  out=acquisition_values)

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from .acquisition import select_indices
+from .acquisition import select_indices, update_hypervolume_improvement_exact
 from .config import (DEFAULT_BATCH_SIZE, DEFAULT_BETA, DEFAULT_INITIAL_SAMPLES,
                      DEFAULT_LENGTH_SCALE, DEFAULT_PRIOR_MEAN, DEFAULT_PRIOR_VARIANCE,
                      NUMBA_FLOAT_TYPE)
@@ -69,14 +69,26 @@ class DeviceBuffers:
 
 
 def _predict_select(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
-                    buffers: DeviceBuffers, batch_size, evaluated):
-    """The fused predict + acquisition + select step; returns x_next (int64 rows)."""
+                    buffers: DeviceBuffers, batch_size, evaluated, acquisition="sum_ucb",
+                    y_evaluated=None, reference_point=None):
+    """The fused predict + acquisition + select step; returns x_next (int64 rows).
+
+    acquisition "sum_ucb" is the reference's (acquisition.py:89-108, fused top-q);
+    "hvi" replaces the acquisition array with the exact hypervolume improvement of the UCB
+    vectors over the Pareto front of `y_evaluated` above `reference_point` (device scan), then
+    selects with the standalone device top-q."""
     out = {"mu": buffers.mu_objectives, "var": buffers.variance_objectives,
            "std_mu": buffers.std_mu_objectives, "std_var": buffers.std_variance_objectives,
            "ucb": buffers.ucb, "acq": buffers.acquisition_values}
-    q = batch_size if batch_size <= _lib.MAX_TOPQ else 0
+    q = batch_size if batch_size <= _lib.MAX_TOPQ and acquisition == "sum_ucb" else 0
     r = predict_acquire(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
                         outputs=tuple(out), topq=q, out=out)
+    if acquisition == "hvi":
+        update_hypervolume_improvement_exact(buffers.acquisition_values, buffers.ucb, y_evaluated,
+                                             len(y_evaluated), reference_point, prior_mean,
+                                             prior_variance)
+    elif acquisition != "sum_ucb":
+        raise ValueError(f"unknown acquisition {acquisition!r} (expected 'sum_ucb' or 'hvi')")
     if q:
         idx = r["top_idx"].cpu().numpy()
         idx = idx[idx >= 0]
@@ -91,7 +103,8 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
              std_mu_objectives, std_variance_objectives, ucb, acquisition_values, input_space,
              prior_mean, prior_variance, reference_point, n_evaluations, total_samples,
              n_objectives, function, betas, length_scales, batch_size, bounds,
-             callbacks: Optional[List[Callable]] = None) -> Tuple[np.ndarray, np.ndarray, int]:
+             callbacks: Optional[List[Callable]] = None, *,
+             acquisition: str = "sum_ucb") -> Tuple[np.ndarray, np.ndarray, int]:
     """bayesian_optimization.py:51-247 with the reference's argument list.
 
     `kernel_matrices` and the posterior arrays may be HIP tensors (in place) or numpy arrays;
@@ -101,7 +114,8 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
     (including its count quirk, :247).
     """
     dev = require_device()
-    del k_star, reference_point, n_objectives, bounds  # unused, as in the reference
+    del k_star, n_objectives, bounds  # unused, as in the reference (reference_point too, unless
+    #                                   acquisition="hvi", the exact hypervolume improvement)
     cands = input_space if isinstance(input_space, CandidateSet) else CandidateSet.explicit(input_space, dev)
     n_obj = len(prior_mean)
 
@@ -134,7 +148,8 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
         torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         x_next = _predict_select(xd, yd, kinv, cands, prior_mean, prior_variance, length_scales, betas,
-                                 bufs, batch_size, x_vector[:current_eval])
+                                 bufs, batch_size, x_vector[:current_eval], acquisition,
+                                 y_vector[:current_eval], reference_point)
         t3 = time.perf_counter()
         for b_idx, point in enumerate(x_next):
             x_vector[current_eval + b_idx] = point
@@ -171,7 +186,10 @@ class BayesianOptimization:
     """bayesian_optimization.py:250-488 — same constructor, kwargs and methods.
 
     Extra kwargs (not in the reference): ``input_space`` (explicit [M, d] candidates, e.g.
-    a Sobol set, instead of the integer grid) and ``device``.
+    a Sobol set, instead of the integer grid), ``device``, ``acquisition`` ("sum_ucb", the
+    reference's default, or "hvi": exact hypervolume improvement of the UCB vectors over the
+    evaluated Pareto front) and ``reference_point`` (the HVI reference point; the reference
+    fixes it at zeros and never uses it, bayesian_optimization.py:425).
     """
 
     def __init__(self, function: Callable[[np.ndarray], np.ndarray], bounds: List[Tuple[int, int]],
@@ -209,7 +227,11 @@ class BayesianOptimization:
             self.prior_mean = K.compute_prior_mean(self.y_vector, self.n_evaluations, n_objectives)
         if np.all(self.prior_variance == DEFAULT_PRIOR_VARIANCE):
             self.prior_variance = K.compute_prior_variance(self.y_vector, self.n_evaluations, n_objectives)
-        self.reference_point = np.array([0.0] * n_objectives)
+        self.reference_point = np.array(kwargs.get("reference_point", [0.0] * n_objectives),
+                                        dtype=NUMBA_FLOAT_TYPE)
+        self.acquisition = kwargs.get("acquisition", "sum_ucb")
+        if self.acquisition not in ("sum_ucb", "hvi"):
+            raise ValueError(f"unknown acquisition {self.acquisition!r} (expected 'sum_ucb' or 'hvi')")
 
     # the reference's preallocated arrays, materialised on the host on demand
     @property
@@ -241,7 +263,8 @@ class BayesianOptimization:
             reference_point=self.reference_point, n_evaluations=self.n_evaluations,
             total_samples=self.total_samples, n_objectives=self.n_objectives, function=self.function,
             betas=self.betas, length_scales=self.length_scales, batch_size=self.batch_size,
-            bounds=self.bounds, callbacks=self.callbacks if self.callbacks else None)
+            bounds=self.bounds, callbacks=self.callbacks if self.callbacks else None,
+            acquisition=self.acquisition)
 
     def pareto_analysis(self) -> np.ndarray:
         """bayesian_optimization.py:465-488."""

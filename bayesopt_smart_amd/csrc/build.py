@@ -18,7 +18,7 @@ ROOT = os.path.dirname(PKG)
 VARIANT = os.environ.get("BO_BUILD_VARIANT", "")      # ablation builds: e.g. "NOEXP"
 LIB = os.path.join(PKG, f"libbo_amd{('_' + VARIANT.lower().replace(',', '_')) if VARIANT else ''}.so")
 BUILD = os.path.join(HERE, "build" + (("_" + VARIANT.lower()) if VARIANT else ""))
-SOURCES = ["bo_predict.hip", "bo_fit.hip", "bo_select.hip", "bo_misc.hip"]
+SOURCES = ["bo_predict.hip", "bo_fit.hip", "bo_select.hip", "bo_misc.hip", "bo_hvi.hip"]
 HEADERS = ["bo_common.h", os.path.join("..", "..", "include", "bo_amd.h")]
 ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",

@@ -180,6 +180,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("auto", "dense"), default="auto",
                     help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved)")
+    ap.add_argument("--acq", choices=("sum_ucb", "hvi"), default="sum_ucb",
+                    help="sum_ucb = the reference's 'hypervolume improvement' (sum of UCBs, fused top-q); "
+                         "hvi = exact hypervolume improvement over the evaluated Pareto front (extension)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -216,16 +219,57 @@ def main():
     xd = torch.tensor(x, device=dev)
     yd = torch.tensor(y, device=dev)
     kd = torch.tensor(kinv, device=dev)
-    outputs = ("mu", "var", "ucb", "acq") if args.config == "C2" else ("mu", "var", "acq")
+    outputs = ("mu", "var", "ucb", "acq") if args.config == "C2" or args.acq == "hvi" else ("mu", "var", "acq")
     out = {k: torch.empty((per_rank,) if k == "acq" else (n_obj, per_rank), dtype=torch.float64,
                           device=dev) for k in outputs}
     gath_v = torch.empty(world * q, dtype=torch.float64, device=dev)
     gath_i = torch.empty(world * q, dtype=torch.int64, device=dev)
 
+    hvi_ev = []
+    if args.acq == "hvi":
+        # exact HVI: the UCB vectors of this shard against the Pareto front of the evaluated
+        # objectives, reference point below every observation; then the standalone top-q
+        import ctypes
+        from bayesopt_smart_amd.acquisition import hypervolume_boxes
+        ref_pt = y.min(axis=0) - 1.0
+        front_y = y[bo.is_pareto_efficient(y)]
+        exd = torch.tensor(x, device=dev)
+        tv = torch.empty(q, dtype=torch.float64, device=dev)
+        ti = torch.empty(q, dtype=torch.int64, device=dev)
+        sel_ws = torch.empty(lib.bo_select_topq_workspace_size(per_rank, q), dtype=torch.uint8, device=dev)
+        glo = (ctypes.c_int64 * 8)(*((list(cands.lo) if cands.lo else []) + [0] * (8 - len(cands.lo or []))))
+        gsh = (ctypes.c_int64 * 8)(*((list(cands.shape) if cands.shape else []) + [1] * (8 - len(cands.shape or []))))
+        shift = (ctypes.c_double * n_obj)(*pm[:n_obj])
+        scale = (ctypes.c_double * n_obj)(*np.sqrt(pv[:n_obj]))
+        strm = bo.device.stream_handle(dev)
+        n_boxes = [0]
+
+        def step_hvi():
+            bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=outputs, topq=0,
+                               offset=offset, count=per_rank, out=out, device=dev, mode=args.mode)
+            boxes = torch.as_tensor(hypervolume_boxes(front_y, ref_pt), device=dev)
+            n_boxes[0] = boxes.shape[0]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            bo._lib.check(lib.bo_hypervolume_improvement_exact(
+                out["acq"].data_ptr(), out["ucb"].data_ptr(), per_rank, per_rank, n_obj, shift, scale,
+                boxes.data_ptr(), boxes.shape[0], strm), "hvi")
+            e1.record()
+            hvi_ev.append((e0, e1))
+            bo._lib.check(lib.bo_select_topq(
+                out["acq"].data_ptr(), per_rank, cands.kind_code,
+                cands.tensor[offset:].data_ptr() if cands.tensor is not None else None, glo, gsh,
+                cands.dim, offset, exd.data_ptr(), exd.shape[0], q, tv.data_ptr(), ti.data_ptr(),
+                sel_ws.data_ptr(), sel_ws.numel(), strm), "select")
+            return {"top_val": tv, "top_idx": ti}
+
     def step():
-        r = bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=outputs,
-                               topq=q, offset=offset, count=per_rank, out=out, device=dev,
-                               mode=args.mode)
+        if args.acq == "hvi":
+            r = step_hvi()
+        else:
+            r = bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=outputs,
+                                   topq=q, offset=offset, count=per_rank, out=out, device=dev,
+                                   mode=args.mode)
         if world > 1:
             dist.all_gather_into_tensor(gath_v, r["top_val"])
             dist.all_gather_into_tensor(gath_i, r["top_idx"])
@@ -266,6 +310,8 @@ def main():
         total = world * per_rank
         metric = ("candidate-points/sec (GP predict + HVI) at N_train=512, N_cand=1M" if args.config == "C3"
                   else f"candidate-points/sec (GP predict + HVI), BASELINE config {args.config}")
+        if args.acq == "hvi":
+            metric += " [acquisition: exact hypervolume improvement, not the reference's sum of UCBs]"
         res = {
             "metric": metric,
             "value": total / t_step,
@@ -296,7 +342,15 @@ def main():
                          "executed_mfma_frac": fx * per_rank / (k_ms * 1e-3) / 1e12 / PEAK_F64_MATRIX_TFLOPS},
             "selected": [int(i) for i in sel[1]],
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if args.acq == "hvi":
+            torch.cuda.synchronize()
+            hms = float(np.mean([a.elapsed_time(b) for a, b in hvi_ev[-args.steps:]]))
+            hb = (8 * n_obj + 8) * per_rank
+            res["hvi_scan"] = {"kernel": f"hvi_exact_kernel<{n_obj}>", "ms": hms, "n_boxes": n_boxes[0],
+                               "front_points": int(front_y.shape[0]),
+                               "bytes_per_candidate": 8 * n_obj + 8, "achieved_GBps": hb / (hms * 1e-3) / 1e9,
+                               "hbm_frac": hb / (hms * 1e-3) / 1e9 / 8000.0}
+        if world == 1 and not args.no_cpu_baseline and args.acq == "sum_ucb":
             if cand[0] == "grid":
                 side = cand[2]
 

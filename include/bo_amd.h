@@ -182,6 +182,28 @@ size_t bo_select_topq_workspace_size(int64_t n_cand, int32_t topq);
  * y: device [n][n_obj] row-major; mask: device uint8 [n]. Bit-exact. */
 int bo_pareto_mask(const double* y, int64_t n, int32_t n_obj, uint8_t* mask, void* stream);
 
+/* Exact hypervolume improvement (opt-in acquisition; the reference's
+ * update_hypervolume_improvement, acquisition.py:89-108, is the sum of UCBs above and stays the
+ * default).  The reference point it would use is bayesian_optimization.py:65 / :425 (unused
+ * there).  Maximisation.
+ *
+ * bo_hvi_boxes (HOST, synchronous, no device memory): decomposes the region above ref_point not
+ * dominated by `front` (host [n][n_obj] row-major; rows with NaN / not strictly above ref_point
+ * are ignored, dominated rows are harmless) into disjoint boxes, host [*][2 n_obj]
+ * (lower[n_obj], upper[n_obj]; upper may be +inf).  Writes the count to *n_boxes; returns
+ * BO_ERR_WORKSPACE (count still written) when it exceeds `capacity`.  n_obj <= 4.
+ *
+ * bo_hypervolume_improvement_exact: acq[i] = sum_b prod_k max(0, min(p_k, upper_bk) - lower_bk)
+ * = HV(front u {p}) - HV(front), p_k = shift[k] + scale[k] * ucb[k][i] (ucb device
+ * [n_obj][ld], the standardised UCB; shift = prior mean, scale = sqrt(prior variance) give
+ * mu + beta sigma in objective units).  boxes: device copy of bo_hvi_boxes' output.  NaN in p
+ * gives NaN (selected first, as NaN is by the reference's argsort).  shift/scale host. */
+int bo_hvi_boxes(const double* front, int64_t n, int32_t n_obj, const double* ref_point,
+                 double* boxes, int64_t capacity, int64_t* n_boxes);
+int bo_hypervolume_improvement_exact(double* acq, const double* ucb, int64_t ld, int64_t n,
+                                     int32_t n_obj, const double* shift, const double* scale,
+                                     const double* boxes, int64_t n_boxes, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * GP fit on device.
  * ---------------------------------------------------------------------------------- */

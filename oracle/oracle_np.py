@@ -283,3 +283,43 @@ def grid_points(bounds):
     ranges = [np.arange(b[0], b[1]) for b in bounds]
     mesh = np.meshgrid(*ranges, indexing="ij")
     return np.stack([m.ravel() for m in mesh], axis=-1)
+
+
+# ------------------------------------------------------- exact hypervolume improvement
+# The reference names a hypervolume-improvement acquisition with a reference point
+# (bayesian_optimization.py:65, :425; acquisition.py:89-108) but computes the sum of UCBs, so
+# nothing in the reference pins the exact HVI: PARITY UNPINNED by the reference.  These two
+# functions are an independent brute-force statement (recursive slicing over the last
+# objective, no box decomposition) that the library's box decomposition and device kernel
+# are checked against on small fronts.
+def hypervolume(points, ref_point):
+    """Volume of the union of boxes [ref, p] over rows p (maximisation).  Rows with NaN or not
+    strictly above ref on every axis add nothing.  O(P^m): small fronts only."""
+    p = np.asarray(points, dtype=np.float64).reshape(-1, len(ref_point))
+    r = np.asarray(ref_point, dtype=np.float64)
+    keep = np.all(np.isfinite(p), axis=1) & np.all(p > r, axis=1)
+    p = p[keep]
+    if p.shape[0] == 0:
+        return 0.0
+    m = p.shape[1]
+    if m == 1:
+        return float(p[:, 0].max() - r[0])
+    # slabs of the last objective between consecutive distinct values, top down: the slab
+    # (z_next, z] is covered by the (m-1)-dim union of the rows with last >= z
+    z = np.unique(p[:, -1])[::-1]
+    vol = 0.0
+    for t, zt in enumerate(z):
+        lower = z[t + 1] if t + 1 < len(z) else r[-1]
+        vol += (zt - lower) * hypervolume(p[p[:, -1] >= zt, :-1], r[:-1])
+    return float(vol)
+
+
+def hypervolume_improvement_exact(points, front, ref_point):
+    """HV(front u {p}) - HV(front) per row p of `points`; NaN rows give NaN."""
+    pts = np.asarray(points, dtype=np.float64)
+    f = np.asarray(front, dtype=np.float64).reshape(-1, len(ref_point))
+    base = hypervolume(f, ref_point)
+    out = np.empty(pts.shape[0])
+    for i, q in enumerate(pts):
+        out[i] = np.nan if np.isnan(q).any() else hypervolume(np.vstack([f, q[None]]), ref_point) - base
+    return out

@@ -1,0 +1,127 @@
+"""Exact hypervolume improvement (opt-in acquisition; not in the reference, which computes the
+sum of UCBs under that name, acquisition.py:89-108).  PARITY UNPINNED by the reference: the
+library's box decomposition (host, bo_hvi_boxes) and the device scan
+(bo_hypervolume_improvement_exact) are checked against an independent brute-force statement,
+oracle_np.hypervolume (recursive slicing), on small fronts with ties, duplicates, points below
+the reference point and NaN rows."""
+import numpy as np
+import pytest
+
+from oracle import oracle_np as O
+
+HVI_RTOL = 1e-9
+
+
+def _front(rng, n, m, kind):
+    if kind == "cont":
+        y = rng.normal(size=(n, m)) * 3.0 + 1.0
+    else:   # integer-valued: heavy ties and duplicates
+        y = rng.integers(-2, 6, size=(n, m)).astype(np.float64)
+    if n > 3:
+        y[0] = np.nan
+        y[1] = y[2]
+    return y
+
+
+def _hvi_from_boxes(boxes, pts):
+    m = pts.shape[1]
+    lo, hi = boxes[:, :m], boxes[:, m:]
+    ext = np.minimum(pts[:, None, :], hi[None]) - lo[None]
+    return np.prod(np.maximum(ext, 0.0), axis=2).sum(axis=1)
+
+
+def _cases():
+    for m in (1, 2, 3, 4):
+        for n in (0, 1, 5, 17):
+            for kind in ("cont", "int"):
+                if m == 4 and n > 5:
+                    continue
+                yield m, n, kind
+
+
+def _tol(ref, pts, r):
+    scale = np.prod(np.maximum(pts - r, 0.0), axis=1) + 1.0
+    return HVI_RTOL * scale
+
+
+@pytest.mark.parametrize("m,n,kind", list(_cases()))
+def test_boxes_match_bruteforce_hvi(m, n, kind):
+    from bayesopt_smart_amd.acquisition import hypervolume_boxes
+    rng = np.random.default_rng(100 * m + n)
+    front = _front(rng, n, m, kind)
+    r = np.full(m, -1.0)
+    pts = rng.normal(size=(40, m)) * 3.0 + 1.5
+    pts[:5] = np.round(pts[:5])           # on the front's integer coordinates
+    if n:
+        pts[5] = front[-1]                 # exactly a front point: HVI 0
+    boxes = hypervolume_boxes(front, r)
+    got = _hvi_from_boxes(boxes, pts)
+    ref = O.hypervolume_improvement_exact(pts, front, r)
+    assert np.all(np.abs(got - ref) <= _tol(ref, pts, r)), np.max(np.abs(got - ref))
+    # the boxes are disjoint and cover the non-dominated region: a huge point's HVI is its box
+    # volume minus HV(front)
+    big = np.full((1, m), 50.0)
+    assert abs(_hvi_from_boxes(boxes, big)[0] - (51.0 ** m - O.hypervolume(front, r))) <= 1e-9 * 51.0 ** m
+
+
+def test_boxes_empty_front_and_capacity():
+    from bayesopt_smart_amd.acquisition import hypervolume_boxes
+    b = hypervolume_boxes(np.zeros((0, 3)), np.zeros(3))
+    assert b.shape == (1, 6) and np.all(b[0, :3] == 0) and np.all(np.isinf(b[0, 3:]))
+    # fronts that need more boxes than the first capacity guess (retry path)
+    rng = np.random.default_rng(3)
+    t = rng.uniform(0, np.pi / 2, size=60)
+    f = np.stack([np.cos(t), np.sin(t), np.cos(2 * t) + 1.1], axis=1)
+    b = hypervolume_boxes(f, np.zeros(3))
+    assert b.shape[0] > 1024
+    pts = rng.uniform(0, 1.5, size=(25, 3))
+    ref = O.hypervolume_improvement_exact(pts, f, np.zeros(3))
+    assert np.allclose(_hvi_from_boxes(b, pts), ref, rtol=0, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [2, 3, 4])
+def test_device_hvi_matches_bruteforce(m):
+    import torch
+    from bayesopt_smart_amd.acquisition import hypervolume_improvement_exact
+    rng = np.random.default_rng(m)
+    front = _front(rng, 12, m, "int")
+    r = np.zeros(m)
+    pm = rng.normal(size=m)
+    pv = rng.uniform(0.5, 4.0, size=m)
+    n = 3000
+    ucb = rng.normal(size=(m, n)) * 2.0
+    ucb[:, 7] = np.nan
+    acq = hypervolume_improvement_exact(torch.as_tensor(ucb, device="cuda"), front, r, pm, pv)
+    got = acq.cpu().numpy()
+    pts = (pm[:, None] + np.sqrt(pv)[:, None] * ucb).T
+    sub = np.r_[np.arange(0, 40), rng.choice(n, 60, replace=False)]
+    ref = O.hypervolume_improvement_exact(pts[sub], front, r)
+    assert np.isnan(got[7]) and np.isnan(ref[np.where(sub == 7)[0][0]])
+    ok = ~np.isnan(ref)
+    assert np.all(np.abs(got[sub][ok] - ref[ok]) <= _tol(ref[ok], pts[sub][ok], r))
+
+
+@pytest.mark.gpu
+def test_device_hvi_full_scan_properties():
+    """Full C3-sized scan: HVI >= 0, zero for UCB vectors the front dominates, equal to the box
+    volume above r when the front is empty, and the in-place update over the loop's arrays."""
+    import torch
+    from bayesopt_smart_amd.acquisition import (hypervolume_improvement_exact,
+                                                update_hypervolume_improvement_exact)
+    rng = np.random.default_rng(11)
+    n, m = 1 << 20, 2
+    ucb = torch.as_tensor(rng.normal(size=(m, n)), device="cuda")
+    pm, pv = np.zeros(m), np.ones(m)
+    front = np.array([[1.0, 2.0], [2.0, 1.0], [0.5, 2.5]])
+    acq = hypervolume_improvement_exact(ucb, front, np.full(m, -3.0), pm, pv).cpu().numpy()
+    u = ucb.cpu().numpy().T
+    assert np.all(acq >= 0)
+    dominated = ((u[:, None, :] <= front[None]).all(axis=2)).any(axis=1)
+    assert np.all(acq[dominated] == 0)
+    empty = hypervolume_improvement_exact(ucb, np.zeros((0, m)), np.full(m, -3.0), pm, pv).cpu().numpy()
+    assert np.allclose(empty, np.prod(np.maximum(u + 3.0, 0), axis=1), rtol=1e-12, atol=0)
+    y = np.vstack([front, [[-1.0, -1.0]]])
+    out = torch.zeros(n, dtype=torch.float64, device="cuda")
+    update_hypervolume_improvement_exact(out, ucb, y, 4, np.full(m, -3.0), pm, pv)
+    assert np.array_equal(out.cpu().numpy(), acq)
