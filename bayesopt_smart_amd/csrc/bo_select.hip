@@ -106,8 +106,25 @@ struct SelArgs {
   const void* cand;
   long long grid_lo[BO_MAX_DIM], grid_shape[BO_MAX_DIM];
   const double* excl;
+  const uint32_t* bitmap;   // grid kind: bit j set iff local candidate j is excluded (else NULL)
   TopEntry* partial;
 };
+
+// Grid kind: mark the evaluated points that lie on this shard of the grid in a bitmap over the
+// shard's local indices (a point equals a grid candidate iff every coordinate is the integer
+// lo_k + v_k with 0 <= v_k < shape_k: the reference's all-d `==`, acquisition.py:137-139).
+__global__ void excl_bitmap_kernel(uint32_t* __restrict__ bm, SelArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n_excl) return;
+  long long lin = 0;
+  for (int k = 0; k < a.dim; ++k) {
+    const double v = a.excl[(long long)e * a.dim + k] - (double)a.grid_lo[k];
+    if (!(v >= 0.0) || v >= (double)a.grid_shape[k] || v != floor(v)) return;
+    lin = lin * a.grid_shape[k] + (long long)v;
+  }
+  const long long j = lin - a.cand_offset;
+  if (j >= 0 && j < a.n_cand) atomicOr(bm + (j >> 5), 1u << (j & 31));
+}
 
 __device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int k) {
   if (a.kind == BO_CAND_I64) return (double)((const long long*)a.cand)[j * a.dim + k];
@@ -135,6 +152,18 @@ __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
     double v = -__builtin_inf();
     long long gi = -1;
     if (j < a.n_cand) {
+      v = a.acq[j];
+      gi = a.cand_offset + j;
+    }
+    // the O(n_excl) exclusion test only for candidates that beat the wave's current q-th entry
+    // (the others cannot enter the list whether excluded or not); after the first steps of the
+    // grid-stride almost no wave-step needs it
+    const double tv = __shfl(lv, a.topq - 1, 64);
+    const long long ti = __shfl(li, a.topq - 1, 64);
+    const bool need = a.n_excl > 0 && gi >= 0 && bo_better(v, gi, tv, ti);
+    if (a.bitmap) {
+      if (gi >= 0 && ((a.bitmap[j >> 5] >> (j & 31)) & 1u)) gi = -1;
+    } else if (__ballot(need) != 0ull && need) {
       double c[BO_MAX_DIM];
       for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
       bool hit = false;
@@ -143,8 +172,7 @@ __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
         for (int k = 0; k < a.dim; ++k) eq = eq && (exs[e * a.dim + k] == c[k]);
         hit = eq;
       }
-      v = a.acq[j];
-      gi = hit ? -1 : a.cand_offset + j;
+      if (hit) gi = -1;
     }
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
@@ -318,8 +346,9 @@ int bo_update_hypervolume_improvement(double* acq, const double* ucb, int32_t n_
 }
 
 size_t bo_select_topq_workspace_size(int64_t n_cand, int32_t topq) {
-  (void)n_cand;
-  return (size_t)1024 * 4 * (topq > 0 ? topq : 1) * sizeof(TopEntry);
+  const size_t lists = (size_t)1024 * 4 * (topq > 0 ? topq : 1) * sizeof(TopEntry);
+  const size_t bits = ((size_t)(n_cand > 0 ? n_cand : 0) + 31) / 32 * 4;
+  return lists + (bits + 255) / 256 * 256;
 }
 
 int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* cand,
@@ -352,8 +381,16 @@ int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* 
     }
   a.excl = excl;
   a.partial = (TopEntry*)ws;
+  if (kind == BO_CAND_GRID && n_excl > 0 && n_cand > 0) {
+    uint32_t* bm = (uint32_t*)((char*)ws + (size_t)1024 * 4 * topq * sizeof(TopEntry));
+    BO_CHECK_HIP(hipMemsetAsync(bm, 0, ((size_t)n_cand + 31) / 32 * 4, s));
+    hipLaunchKernelGGL(excl_bitmap_kernel, dim3((unsigned)((n_excl + 255) / 256)), dim3(256), 0, s, bm, a);
+    BO_CHECK_HIP(hipGetLastError());
+    a.bitmap = bm;
+  }
   long long blocks = (n_cand + 255) / 256;
-  const int max_blocks = cus_count() * 4 < 1024 ? cus_count() * 4 : 1024;
+  // one workgroup per CU: an HBM-bound pass of 8 B per candidate; fewer lists for the merge
+  const int max_blocks = cus_count() < 1024 ? cus_count() : 1024;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(select_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
