@@ -531,6 +531,46 @@ struct KRows {
   }
 };
 
+// Next-chunk generation split into three stages that chunk_step places between the MFMA
+// pairs of the chunk's first E-pair (sched barriers pin them), so that every LDS round trip
+// of the generation (SEP: row factor + table index, then the table value; the alpha values
+// of the mean) completes under MFMAs instead of stalling the wave before the chunk:
+//   s0: rv[f], rb[f], alpha[f] loads     s1: table loads T[rb - jl]     s2: the products.
+// The exp path (!SEP) is VALU work that serialises with f64 MFMAs anyway: all of it in s2.
+template <int DIM, bool SEP>
+struct KGen {
+  double rv[8], tv[8];
+  int rb[8];
+  __device__ __forceinline__ void s0(const KRows<DIM, SEP>& K, const double* al, bool mu_on, int ch,
+                                     int g, double (&A)[8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int f = 32 * ch + 4 * s + g;
+      const double a = al[f];
+      A[s] = mu_on ? a : 0.0;
+      if (SEP) { rv[s] = K.rv[f]; rb[s] = K.rb[f]; }
+    }
+  }
+  __device__ __forceinline__ void s1(const KRows<DIM, SEP>& K) {
+    if (SEP) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) tv[s] = K.tb[rb[s] - K.jl];
+    }
+  }
+  __device__ __forceinline__ void s2(const KRows<DIM, SEP>& K, int ch, int g, double (&B)[8]) {
+#ifdef BO_ABL_NOGEN
+    K.chunk(ch, g, B);
+    return;
+#endif
+    if (SEP) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) B[s] = rv[s] * tv[s];
+    } else {
+      K.chunk(ch, g, B);
+    }
+  }
+};
+
 template <int DIM, bool SEP, bool UPPER>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   constexpr bool upper = UPPER;
@@ -639,14 +679,15 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
           acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
         }
-        // one chunk: MFMAs from register set B while the next chunk's K* is generated into
-        // Bn (the two sets alternate: no register copies between the chunks)
-        auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8]) {
-          if (ch + 1 < nch) K.chunk(ch + 1, g, Bn);             // next chunk, in the MFMA shadow
-          if (e0 == 0) {
-#pragma unroll
-            for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * ch + 4 * s + g], B[s], mpart);
-          }
+        // one chunk: MFMAs from register set B while the next chunk's K* (and its alpha
+        // values, An) is generated into Bn in three stages inside E-pair 0's MFMA stream (the
+        // sets alternate: no register copies between the chunks).  Branch-free: the last chunk
+        // regenerates itself (chn clamped) and groups after the first add 0 x alpha to mu.
+        const bool mu_on = e0 == 0;
+        KGen<DIM, SEP> gen;
+        auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8], const double (&A)[8],
+                              double (&An)[8]) {
+          const int chn = ch + 1 < nch ? ch + 1 : ch;
           // the group's E-pairs touching chunk ch, ascending: the first n_here of them (e0 + e
           // <= ch when upper).  EpChain nests the guards (body e+1 is reached only from body e),
           // so every body has one predecessor and hipcc's vmcnt waits inside the chunk stay
@@ -655,6 +696,10 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           const int n_here = upper ? (ch - e0 + 1 < eN ? ch - e0 + 1 : eN) : eN;
           auto ep_body = [&](auto e_c) {
             constexpr int e = decltype(e_c)::value;
+            if constexpr (e == 0) {
+              gen.s0(K, al, mu_on, chn, g, An);
+              __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int pp = 0; pp < 4; ++pp) {
               // MFMAs first, then the refill of the same ring slot (no operand copies)
@@ -670,19 +715,37 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               asm volatile("" : "+v"(wa[pp]), "+v"(wb[pp]) : "s"(so));
 #endif
               ++pos;
+              if constexpr (e == 0) {
+                if (pp == 0) {
+                  __builtin_amdgcn_sched_barrier(0);
+                  gen.s1(K);
+                  __builtin_amdgcn_sched_barrier(0);
+                } else if (pp == 1) {
+                  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                  for (int s = 0; s < 8; ++s) mpart = __builtin_fma(A[s], B[s], mpart);
+                  __builtin_amdgcn_sched_barrier(0);
+                } else if (pp == 2) {
+                  __builtin_amdgcn_sched_barrier(0);
+                  gen.s2(K, chn, g, Bn);
+                  __builtin_amdgcn_sched_barrier(0);
+                }
+              }
             }
           };
           EpChain<0, kCMaxEp>::run(ep_body, n_here);
         };
         const int c0 = upper ? e0 : 0;
-        double BX[8], BY[8];
+        double BX[8], BY[8], AX[8], AY[8];
         K.chunk(c0, g, BX);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) AX[s] = mu_on ? al[32 * c0 + 4 * s + g] : 0.0;
         int ch = c0;
         for (; ch + 1 < nch; ch += 2) {
-          chunk_step(ch, BX, BY);
-          chunk_step(ch + 1, BY, BX);
+          chunk_step(ch, BX, BY, AX, AY);
+          chunk_step(ch + 1, BY, BX, AY, AX);
         }
-        if (ch < nch) chunk_step(ch, BX, BY);
+        if (ch < nch) chunk_step(ch, BX, BY, AX, AY);
         // q = k . z (dense) or 2 k . (U k) (upper) with the rows 32 ep + g + 4r (+16) of K* =
         // chunk ep's slots r (4 + r), regenerated here (no branch inside the MFMA stream: a
         // branch join there costs a vmcnt(0) drain of the W ring).  A full fence per
