@@ -551,6 +551,17 @@ struct KGen {
       if (SEP) { rv[s] = K.rv[f]; rb[s] = K.rb[f]; }
     }
   }
+  // s0 without the alpha values (the variance epilogue's regeneration)
+  __device__ __forceinline__ void s0k(const KRows<DIM, SEP>& K, int ch, int g) {
+    if (SEP) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int f = 32 * ch + 4 * s + g;
+        rv[s] = K.rv[f];
+        rb[s] = K.rb[f];
+      }
+    }
+  }
   __device__ __forceinline__ void s1(const KRows<DIM, SEP>& K) {
     if (SEP) {
 #pragma unroll
@@ -750,16 +761,28 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         // chunk ep's slots r (4 + r), regenerated here (no branch inside the MFMA stream: a
         // branch join there costs a vmcnt(0) drain of the W ring).  A full fence per
         // accumulator: the scheduler may sink any E-pair's last MFMAs down to its own fence.
+        // Software-pipelined: E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence
+        // and multiplied after its FMAs, so the fences' wait states cover the LDS round trips.
+        {
+          KGen<DIM, SEP> gq[2];
+          double S[2][8];
+          gq[0].s0k(K, e0, g);
+          gq[0].s1(K);
+          gq[0].s2(K, e0, g, S[0]);
 #pragma unroll
-        for (int e = 0; e < kCMaxEp; ++e) {
-          if (e < eN) {
-            mfma_fence<true, 64>(acc[e][0], acc[e][1]);
-            double S[8];
-            K.chunk(e0 + e, g, S);
+          for (int e = 0; e < kCMaxEp; ++e) {
+            if (e < eN) {
+              const int cur = e & 1, nxt = cur ^ 1;
+              const bool more = e + 1 < eN;
+              if (more) gq[nxt].s0k(K, e0 + e + 1, g);
+              mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+              if (more) gq[nxt].s1(K);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              qpart = __builtin_fma(S[r], acc[e][0][r], qpart);
-              qpart = __builtin_fma(S[4 + r], acc[e][1][r], qpart);
+              for (int r = 0; r < 4; ++r) {
+                qpart = __builtin_fma(S[cur][r], acc[e][0][r], qpart);
+                qpart = __builtin_fma(S[cur][4 + r], acc[e][1][r], qpart);
+              }
+              if (more) gq[nxt].s2(K, e0 + e + 1, g, S[nxt]);
             }
           }
         }
