@@ -698,7 +698,8 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         KGen<DIM, SEP> gen;
         auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8], const double (&A)[8],
                               double (&An)[8]) {
-          const int chn = ch + 1 < nch ? ch + 1 : ch;
+          // next chunk: ascending (dense) / descending (upper); the last one regenerates itself
+          const int chn = upper ? (ch > e0 ? ch - 1 : ch) : (ch + 1 < nch ? ch + 1 : ch);
           // the group's E-pairs touching chunk ch, ascending: the first n_here of them (e0 + e
           // <= ch when upper).  EpChain nests the guards (body e+1 is reached only from body e),
           // so every body has one predecessor and hipcc's vmcnt waits inside the chunk stay
@@ -707,6 +708,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           const int n_here = upper ? (ch - e0 + 1 < eN ? ch - e0 + 1 : eN) : eN;
           auto ep_body = [&](auto e_c) {
             constexpr int e = decltype(e_c)::value;
+            (void)B;
             if constexpr (e == 0) {
               gen.s0(K, al, mu_on, chn, g, An);
               __builtin_amdgcn_sched_barrier(0);
@@ -743,27 +745,51 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
                 }
               }
             }
+            // upper: E-pair e0 + e is complete after its own chunk (chunks descend), the last
+            // body of that chunk: q += K*[chunk rows] . acc with the rows still in B (rows
+            // 32 ep + g + 4r (+16) = B slots r (4 + r)); no regeneration
+            if constexpr (UPPER) {
+              if (ch - e0 == e) {
+                mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  qpart = __builtin_fma(B[r], acc[e][0][r], qpart);
+                  qpart = __builtin_fma(B[4 + r], acc[e][1][r], qpart);
+                }
+              }
+            }
           };
           EpChain<0, kCMaxEp>::run(ep_body, n_here);
         };
-        const int c0 = upper ? e0 : 0;
+        const int c0 = upper ? nch - 1 : 0;
         double BX[8], BY[8], AX[8], AY[8];
         K.chunk(c0, g, BX);
 #pragma unroll
         for (int s = 0; s < 8; ++s) AX[s] = mu_on ? al[32 * c0 + 4 * s + g] : 0.0;
         int ch = c0;
-        for (; ch + 1 < nch; ch += 2) {
-          chunk_step(ch, BX, BY, AX, AY);
-          chunk_step(ch + 1, BY, BX, AY, AX);
+        if (upper) {
+          for (; ch - 1 >= e0; ch -= 2) {
+            chunk_step(ch, BX, BY, AX, AY);
+            chunk_step(ch - 1, BY, BX, AY, AX);
+          }
+          if (ch >= e0) chunk_step(ch, BX, BY, AX, AY);
+        } else {
+          for (; ch + 1 < nch; ch += 2) {
+            chunk_step(ch, BX, BY, AX, AY);
+            chunk_step(ch + 1, BY, BX, AY, AX);
+          }
+          if (ch < nch) chunk_step(ch, BX, BY, AX, AY);
         }
-        if (ch < nch) chunk_step(ch, BX, BY, AX, AY);
-        // q = k . z (dense) or 2 k . (U k) (upper) with the rows 32 ep + g + 4r (+16) of K* =
-        // chunk ep's slots r (4 + r), regenerated here (no branch inside the MFMA stream: a
-        // branch join there costs a vmcnt(0) drain of the W ring).  A full fence per
-        // accumulator: the scheduler may sink any E-pair's last MFMAs down to its own fence.
-        // Software-pipelined: E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence
-        // and multiplied after its FMAs, so the fences' wait states cover the LDS round trips.
-        {
+        // q = k . z (dense): the rows 32 ep + g + 4r (+16) of K* = chunk ep's slots r (4 + r),
+        // regenerated here (the upper form's q was accumulated inside the chunk loop).  A full
+        // fence per accumulator: the scheduler may sink any E-pair's last MFMAs down to it.
+#ifdef BO_ABL_STAMPS
+        STAMP(t_b); st_sum[1] += t_b - t_a; t_a = t_b;   // chunk loop (MFMAs)
+#endif
+        // dense: q = k . z after the last chunk, chunk ep's K* regenerated.  Software-pipelined:
+        // E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence and multiplied after
+        // its FMAs, so the fences' wait states cover the LDS round trips.
+        if (!upper) {
           KGen<DIM, SEP> gq[2];
           double S[2][8];
           gq[0].s0k(K, e0, g);
@@ -789,7 +815,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       }
       if (upper) qpart *= 2.0;
 #ifdef BO_ABL_STAMPS
-      STAMP(t_b); st_sum[1] += t_b - t_a; t_a = t_b;   // chunk loop (MFMAs) + epilogue
+      STAMP(t_b); st_sum[2] += t_b - t_a; t_a = t_b;   // variance epilogue
 #endif
       qpart += __shfl_xor(qpart, 16, 64);
       qpart += __shfl_xor(qpart, 32, 64);
@@ -900,7 +926,8 @@ __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ 
     const int which = (int)(r & 1); r >>= 1;
     const int pp = (int)(r & 3); r >>= 2;
     // r = block index: groups of kCMaxEp E-pairs in order; within a group chunks c
-    // ascending, within a chunk the group's E-pairs ascending (ep <= c when upper)
+    // ascending (dense) or descending (upper), within a chunk the group's E-pairs ascending
+    // (ep <= c when upper)
     int e0 = 0;
     for (;; e0 += kCMaxEp) {
       const long long nb = cm_group_blocks(nch, e0, upper);
@@ -912,15 +939,21 @@ __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ 
     if (!upper) {
       c = (int)(r / eN);
       el = (int)(r % eN);
-    } else if (r < (long long)(eN - 1) * eN / 2) {           // partial chunks: 1, 2, ... blocks
-      int sz = 1;
-      while (r >= sz) { r -= sz; ++sz; }
-      c = e0 + sz - 1;
-      el = (int)r;
     } else {
-      r -= (long long)(eN - 1) * eN / 2;
-      c = e0 + eN - 1 + (int)(r / eN);
-      el = (int)(r % eN);
+      // upper: chunks DESCENDING (E-pair ep is complete after chunk ep, whose K* is then still
+      // in the kernel's registers): full chunks c = nch-1 .. e0+eN-1 (eN blocks each), then
+      // partial chunks c = e0+eN-2 .. e0 (eN-1, ..., 1 blocks)
+      const long long full = (long long)(nch - (e0 + eN - 1)) * eN;
+      if (r < full) {
+        c = nch - 1 - (int)(r / eN);
+        el = (int)(r % eN);
+      } else {
+        r -= full;
+        int sz = eN - 1;
+        while (r >= sz) { r -= sz; --sz; }
+        c = e0 + sz - 1;
+        el = (int)r;
+      }
     }
     const int ep = e0 + el;
     const int row = 16 * (2 * ep + which) + (lane & 15);
