@@ -85,6 +85,7 @@ struct FusedArgs {
   int sep_S;
   long long sep_lo;
   int off_tbl, off_rw;
+  int rw_cache;                          // SEP row factors kept for every objective (LDS permitting)
 };
 
 template <int DIM>
@@ -511,7 +512,7 @@ struct EpChain<N, N> {
 template <int DIM, bool SEP>
 struct KRows {
   const double* rv;   // SEP: [n_pad] pv * R(f) (0 for padded rows)
-  const int* rb;      // SEP: [n_pad] table index base x_f,last - c0_last + S - 1
+  const int* rb;      // SEP: [n_pad] table index base (x_f,last - lo_last) + S - 1; jl = col0 + lane
   const double* tb;   // SEP: objective's table T
   const double* xs;   // !SEP: training rows [n_pad][DIM] (padded rows at 1e200)
   double c[DIM];      // !SEP: this lane's candidate
@@ -591,8 +592,15 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   const double* tbl = smem + a.off_tbl;                     // [n_obj][2S - 1]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, jl = lane & 15;
-  double* rv = smem + a.off_rw + (size_t)wave * a.n_pad * 2;   // per wave: rv[n_pad], rb[n_pad]
-  int* rb = (int*)(rv + a.n_pad);
+  // SEP row factors, per wave: rv[nslot][n_pad] = pv_o R(f) (one slot per objective when they
+  // are cached across the tiles of a grid row, else one slot rebuilt per objective and tile),
+  // then rb[n_pad] = table index base (x_f,last - lo_last) + S - 1 and on[n_pad] = "training
+  // point f lies on this grid row" (all other coordinates equal)
+  const int nslot = a.rw_cache ? a.n_obj : 1;
+  double* rv = smem + a.off_rw + (size_t)wave * a.n_pad * (nslot + 1);
+  int* rb = (int*)(rv + (size_t)nslot * a.n_pad);
+  int* on = rb + a.n_pad;
+  long long cur_row = -1;
   const int TS = 2 * a.sep_S - 1;
   const int nch = a.n_pad / 32;
   const int last = a.dim - 1;
@@ -608,18 +616,55 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   unsigned long long t_a = 0, t_b = 0;
   STAMP(t_a);
 #endif
-  for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+  // SEP: contiguous tile ranges per workgroup, so that a wave walks along grid rows and its
+  // row factors are rebuilt once per row (every S / 64 tiles) instead of once per tile;
+  // otherwise grid-strided tiles
+  const long long tpw = (a.n_tiles + gridDim.x - 1) / gridDim.x;
+  const long long t_first = SEP ? blockIdx.x * tpw : blockIdx.x;
+  const long long t_end = SEP ? (t_first + tpw < a.n_tiles ? t_first + tpw : a.n_tiles) : a.n_tiles;
+  const long long t_step = SEP ? 1 : gridDim.x;
+  // row pass (numba_kernels.py:436-442 split along the grid): per training row f, the squared
+  // distance over the non-last coordinates is shared by the wave's 16 candidates
+  auto row_pass = [&](const double (&c)[DIM], int o_lo, int o_hi) {
+    __builtin_amdgcn_wave_barrier();
+    for (int f = lane; f < a.n_pad; f += 64) {
+      int b = a.sep_S - 1, onrow = 0;                      // padded rows: any in-range index, v = 0
+      double sqs = 0.0;
+      if (f < a.n_train) {
+        const double* r = xs + f * DIM;
+        double xl = 0.0;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) {
+          if (k == last) xl = r[k];
+          else { const double d = r[k] - c[k]; sqs = __builtin_fma(d, d, sqs); }
+        }
+        b = (int)(xl - (double)a.sep_lo) + a.sep_S - 1;
+        onrow = sqs == 0.0;
+      }
+      for (int o = o_lo; o < o_hi; ++o)
+        rv[(size_t)(o - o_lo) * a.n_pad + f] = f < a.n_train ? a.pv[o] * exp(sqs * a.nhl[o]) : 0.0;
+      rb[f] = b;
+      on[f] = onrow;
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (long long tile = t_first; tile < t_end; tile += t_step) {
     const long long j = tile * kTile + wave * 16 + jl;
     const bool valid = j < a.n_cand;
     double c[DIM];
-    double c0_last = 0.0;
+    int col0 = 0;                 // SEP: the wave's first candidate's offset on the last axis
     if (SEP) {
       // the wave's 16 candidates: one grid row, consecutive along the last axis
       const long long j0 = tile * kTile + wave * 16;
-      load_candidate<DIM>(a, j0 < a.n_cand ? j0 : 0, true, c);
+      const long long jj = j0 < a.n_cand ? j0 : 0;
+      load_candidate<DIM>(a, jj, true, c);
 #pragma unroll
       for (int k = 0; k < DIM; ++k)
-        if (k == last) { c0_last = c[k]; c[k] += (double)jl; }
+        if (k == last) { col0 = (int)(c[k] - (double)a.sep_lo); c[k] += (double)jl; }
+      if (a.rw_cache) {
+        const long long row = (a.cand_offset + jj) / a.sep_S;
+        if (row != cur_row) { row_pass(c, 0, a.n_obj); cur_row = row; }
+      }
     } else {
       load_candidate<DIM>(a, j, valid, c);
     }
@@ -641,35 +686,13 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
     unsigned int xmask = 0;
     double acq = 0.0;
     for (int o = 0; o < a.n_obj; ++o) {
+      if (SEP && !a.rw_cache) row_pass(c, o, o + 1);
       KRows<DIM, SEP> K;
-      K.rv = rv; K.rb = rb; K.tb = tbl + (size_t)o * TS; K.xs = xs;
-      K.pv = a.pv[o]; K.nhl = a.nhl[o]; K.jl = jl;
+      K.rv = rv + (a.rw_cache ? (size_t)o * a.n_pad : 0); K.rb = rb; K.tb = tbl + (size_t)o * TS;
+      K.xs = xs; K.pv = a.pv[o]; K.nhl = a.nhl[o];
+      K.jl = SEP ? col0 + jl : jl;   // T index = rb[f] - (col0 + jl) = x_f,last - c_last + S - 1
 #pragma unroll
       for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
-      if (SEP) {
-        // row pass: pv R(f) and the table index base of every row (numba_kernels.py:436-442)
-        __builtin_amdgcn_wave_barrier();
-        for (int f = lane; f < a.n_pad; f += 64) {
-          double v = 0.0;
-          int b = a.sep_S - 1 + 15;                          // any in-range index (v = 0)
-          if (f < a.n_train) {
-            const double* r = xs + f * DIM;
-            double sqs = 0.0, xl = 0.0;
-#pragma unroll
-            for (int k = 0; k < DIM; ++k) {
-              if (k == last) xl = r[k];
-              else { const double d = r[k] - c[k]; sqs = __builtin_fma(d, d, sqs); }
-            }
-            v = K.pv * exp(sqs * K.nhl);
-            const int dx = (int)(xl - c0_last);
-            b = dx + a.sep_S - 1;
-            if (o == 0 && sqs == 0.0 && dx >= 0 && dx < 16) xmask |= 1u << dx;
-          }
-          rv[f] = v;
-          rb[f] = b;
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
 #ifdef BO_ABL_STAMPS
       STAMP(t_b); st_sum[0] += t_b - t_a; t_a = t_b;   // tile setup + row pass
 #endif
@@ -840,7 +863,13 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
     if (valid && g == 0 && a.acq) a.acq[j] = acq;
     if (a.topq > 0) {
       if (SEP && !a.excl) {
-        // OR the row-pass bits over the wave; bit jl is this lane's candidate
+        // training points on this grid row whose last coordinate falls in the wave's 16
+        // columns (all coordinates equal: acquisition.py:137-139); OR over the wave, bit jl
+        // is this lane's candidate
+        for (int f = lane; f < a.n_train; f += 64) {
+          const int dx = rb[f] - (a.sep_S - 1) - col0;
+          if (on[f] && dx >= 0 && dx < 16) xmask |= 1u << dx;
+        }
         unsigned int m = xmask;
 #pragma unroll
         for (int sh = 32; sh > 0; sh >>= 1) m |= (unsigned int)__shfl_xor((int)m, sh, 64);
@@ -1098,6 +1127,7 @@ struct Plan {
   bool cm;               // chunk-major kernel (cm_predict_kernel)
   bool sep;              // ... with the integer-grid K* generation
   int off_tbl, off_rw;   // LDS offsets in doubles
+  bool rw_cache;          // SEP row factors cached per objective
   int grid, waves;       // persistent grid, waves per workgroup
   long long n_tiles;
   size_t lds;
@@ -1130,6 +1160,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   // chunk-major kernel (cm_predict_kernel) for N <= 512; on the reference's 'ij' grid with
   // 16-aligned rows it generates K* from per-row factors and an exp table (pl->sep)
   pl->sep = false;
+  pl->rw_cache = false;
   pl->cm = false;
   pl->off_tbl = pl->off_rw = 0;
   if (!kmem) {
@@ -1145,12 +1176,15 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
     if (d->cand_kind == BO_CAND_GRID && !(d->mode & BO_PREDICT_NO_SEPARABLE)) {
       const long long S = d->grid_shape[d->dim - 1];
       const size_t tbl = (size_t)d->n_obj * (2 * S - 1);
-      const size_t lds = base + tbl + (size_t)kWaves * n_pad * 2;
-      if (S % 16 == 0 && S <= 32768 && d->cand_offset % 16 == 0 && lds * sizeof(double) <= 160 * 1024) {
+      // per wave: n_obj (cached) or 1 slot of row factors + the int index / on-row arrays
+      const size_t lds_c = base + tbl + (size_t)kWaves * n_pad * (d->n_obj + 1);
+      const size_t lds_1 = base + tbl + (size_t)kWaves * n_pad * 2;
+      if (S % 16 == 0 && S <= 32768 && d->cand_offset % 16 == 0 && lds_1 * sizeof(double) <= 160 * 1024) {
         pl->sep = true;
+        pl->rw_cache = lds_c * sizeof(double) <= 160 * 1024;
         pl->off_tbl = (int)base;
         pl->off_rw = (int)(base + tbl);
-        pl->lds = lds * sizeof(double);
+        pl->lds = (pl->rw_cache ? lds_c : lds_1) * sizeof(double);
       }
     }
   }
@@ -1338,6 +1372,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.sep_lo = pl.sep ? d->grid_lo[d->dim - 1] : 0;
   fa.off_tbl = pl.off_tbl;
   fa.off_rw = pl.off_rw;
+  fa.rw_cache = pl.rw_cache ? 1 : 0;
   if (pl.sep) {
     BO_CHECK_HIP(hipMemsetAsync(sep_flag, 0, sizeof(int), s));
     hipLaunchKernelGGL(sep_check_kernel, dim3((unsigned)((d->n_train + 255) / 256)), dim3(256), 0, s,
