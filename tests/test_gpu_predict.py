@@ -182,3 +182,42 @@ def test_full_size_c3_properties(bo):
     ref = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv)
     check_predict({k: (out[k][..., sub]) for k in ("mu", "var", "acq")}, ref, pv)
     check_topq(out["top_idx"], out["acq"], excl, 16)
+
+
+@pytest.mark.parametrize("shape,n,n_obj,offset", [
+    ((4, 8, 64), 150, 2, 0),        # 3-D grid: rows keyed by the first two coordinates
+    ((16, 1024), 480, 4, 0),        # 4 objectives: row factors rebuilt per objective (LDS)
+    ((16, 1024), 300, 3, 3 * 1024 + 48),   # shard starting mid-row (offset % 16 == 0)
+])
+def test_predict_grid_row_factor_paths(bo, shape, n, n_obj, offset):
+    """The integer-grid K* path (row factors per grid row, exp table over the last axis) in
+    its cached and per-objective forms, on a 3-D grid and on a shard that starts mid-row,
+    against the oracle on a candidate subsample."""
+    import torch
+    rng = np.random.default_rng(n)
+    total = int(np.prod(shape))
+    lin = rng.choice(total, size=n, replace=False)
+    x = np.stack(np.unravel_index(lin, shape), axis=1).astype(np.float64)
+    y = rng.normal(size=(n, n_obj)) * 30 + 5
+    pm, pv = y.mean(0), y.var(0)
+    ls = rng.uniform(1.5, 2.5, size=n_obj)
+    betas = rng.uniform(0.5, 2.5, size=n_obj)
+    km = np.zeros((n_obj, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    assert max(np.linalg.cond(km[o] + 1e-6 * np.eye(n)) for o in range(n_obj)) < 1e6
+    kinv = O.invert_k(n, km)
+    cands = bo.predict.CandidateSet.grid([(0, s) for s in shape])
+    count = min(total - offset, 8192)
+    res = bo.predict.predict_acquire(x, y, kinv, cands, pm, pv, ls, betas, outputs=("mu", "var", "acq"),
+                                     topq=8, offset=offset, count=count)
+    torch.cuda.synchronize()
+    out = {k: res[k].cpu().numpy() for k in ("mu", "var", "acq", "top_idx")}
+    sub = np.unique(np.r_[np.arange(0, min(count, 300)), rng.choice(count, 700, replace=False)])
+    pts = np.stack(np.unravel_index(offset + sub, shape), axis=1).astype(np.int64)
+    ref = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv)
+    check_predict({"mu": out["mu"][:, sub], "var": out["var"][:, sub], "acq": out["acq"][sub]},
+                  {k: ref[k] for k in ("mu", "var", "acq")}, pv)
+    # top-q over the shard against the shard's full acq array (checked above on the subsample)
+    shard_pts = np.stack(np.unravel_index(offset + np.arange(count), shape), axis=1)
+    excl = _excluded(shard_pts, x)
+    check_topq(out["top_idx"] - offset, out["acq"], excl, 8)
