@@ -88,6 +88,7 @@ _SIGS = {
                                  c_vp]),
     "bo_compute_mll_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
     "bo_selftest_mfma_f64": (C.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "bo_selftest_mfma_f32": (C.c_int, [c_vp, c_vp, c_vp, c_vp]),
     "bo_profile_start": (C.c_int, [C.c_int]),
     "bo_profile_stop": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }

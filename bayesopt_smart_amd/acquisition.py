@@ -118,7 +118,7 @@ def hypervolume_boxes(front, reference_point) -> np.ndarray:
         out = np.empty((cap, 2 * n_obj), dtype=np.float64)
         st = lib.bo_hvi_boxes(f.ctypes.data_as(dp), f.shape[0], n_obj, r.ctypes.data_as(dp),
                               out.ctypes.data, cap, _C.byref(cnt))
-        if st == 3 and cnt.value > cap:      # BO_ERR_WORKSPACE: retry with the reported count
+        if st == _lib.ERR_WORKSPACE and cnt.value > cap:   # retry with the reported count
             cap = int(cnt.value)
             continue
         _lib.check(st, "bo_hvi_boxes")

@@ -1116,6 +1116,257 @@ __global__ void selftest_mfma_kernel(const double* a, const double* b, double* d
   for (int r = 0; r < 4; ++r) d[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
 }
 
+// ---------------------------------------------------------------------------------------
+// fp32 variant (BO_PREDICT_FP32; BASELINE config C5 "fp32 with fp64 reference check"):
+// the upper form q = 2 k.(U k) on v_mfma_f32_16x16x4_f32 (32 cycles per MFMA per SIMD, twice
+// the f64 rate), K* = 2^(nhl log2e |x_f - c_j|^2 + log2 pv) on v_exp_f32, mu / q accumulated
+// in f32 and everything after them (variance floor, standardisation, UCB, sum, top-q) in f64.
+//
+// Body = E-quad: 64 rows of U (4 MFMA row blocks b), chunk = 64 rows of K* (16 k-steps).
+// f32 D layout (lane l holds D[4 (l >> 4) + r][l & 15]) differs from f64's, so the K* row fed
+// at k-step s by lane group g is permuted: f(s, g) = 64 c + 16 (s >> 2) + 4 g + (s & 3).  Then
+// the rows a completing E-quad's accumulator block b holds in its lane (64 ep + 16 b + 4 g + r)
+// are exactly B slots s = 4 b + r of chunk ep: the in-register epilogue of the f64 kernel.
+// Chunks descend (E-quad ep is complete at chunk ep); W streams per (group, chunk, E-quad,
+// k-quad kq, block b) as one 16-B float4 per lane (k-steps 4 kq .. 4 kq + 3), through a
+// 16-entry register ring that holds exactly one E-quad block (static slot indices).
+// Exclusion of evaluated points is tested (exactly, in f64 from HBM) only for candidates that
+// would enter the wave's top-q.
+// ---------------------------------------------------------------------------------------
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kC32MaxEp = 16;   // E-quads per group (1024 rows)
+
+__device__ __forceinline__ f4 mfma32(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 wload32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void mfma_fence32(f4& a, f4& b, f4& c, f4& d) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+               : "+a"(a), "+a"(b), "+a"(c), "+a"(d));
+}
+
+// (chunk, E-quad) blocks of group e0, upper form
+__host__ __device__ inline long long c32_group_blocks(int nch, int e0) {
+  const int eN = nch - e0 < kC32MaxEp ? nch - e0 : kC32MaxEp;
+  return (long long)(eN - 1) * eN / 2 + (long long)(nch - e0 - eN + 1) * eN;
+}
+__host__ __device__ inline long long c32_blocks(int nch) {
+  long long b = 0;
+  for (int e0 = 0; e0 < nch; e0 += kC32MaxEp) b += c32_group_blocks(nch, e0);
+  return b;
+}
+
+// float4 entry (o, block, kq, b, lane) = {W[row][col0 + t], t = 0..3}, row = 64 ep + 16 b +
+// (lane & 15), col0 = 64 c + 16 kq + 4 (lane >> 4); W = triu(sym(K^-1)) with halved diagonal.
+__global__ void pack32_kernel(f4* __restrict__ out, const double* __restrict__ kinv, long long ld,
+                              int n, int n_pad, int n_obj) {
+  const int nch = n_pad / 64;
+  const long long per_obj = c32_blocks(nch) * 1024;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per_obj * n_obj;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(t / per_obj);
+    long long r = t - (long long)o * per_obj;
+    const int lane = (int)(r & 63); r >>= 6;
+    const int b = (int)(r & 3); r >>= 2;
+    const int kq = (int)(r & 3); r >>= 2;
+    int e0 = 0;
+    for (;; e0 += kC32MaxEp) {
+      const long long nb = c32_group_blocks(nch, e0);
+      if (r < nb) break;
+      r -= nb;
+    }
+    const int eN = nch - e0 < kC32MaxEp ? nch - e0 : kC32MaxEp;
+    int c, el;
+    const long long full = (long long)(nch - (e0 + eN - 1)) * eN;
+    if (r < full) {
+      c = nch - 1 - (int)(r / eN);
+      el = (int)(r % eN);
+    } else {
+      r -= full;
+      int sz = eN - 1;
+      while (r >= sz) { r -= sz; --sz; }
+      c = e0 + sz - 1;
+      el = (int)r;
+    }
+    const int row = 64 * (e0 + el) + 16 * b + (lane & 15);
+    const int col0 = 64 * c + 16 * kq + 4 * (lane >> 4);
+    const double* wo = kinv + (long long)o * ld * ld;
+    f4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = col0 + q;
+      double w = 0.0;
+      if (row < n && f < n && f >= row)
+        w = f == row ? 0.5 * wo[(long long)row * ld + row]
+                     : 0.5 * (wo[(long long)row * ld + f] + wo[(long long)f * ld + row]);
+      v[q] = (float)w;
+    }
+    out[(size_t)o * per_obj + (t - (long long)o * per_obj)] = v;
+  }
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem32[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, jl = lane & 15;
+  float* xs = smem32;                                        // [n_pad][DIM]
+  float* al = xs + (size_t)a.n_pad * DIM;                    // [n_obj][n_pad]
+  for (int t = tid; t < a.n_pad * DIM; t += blockDim.x) xs[t] = (float)a.xpad[t];   // 1e200 -> inf
+  for (int t = tid; t < a.n_obj * a.n_pad; t += blockDim.x) al[t] = (float)a.alpha[t];
+  __syncthreads();
+  const int nch = a.n_pad / 64;
+  const long long w_obj = c32_blocks(nch) * 1024 * 16;       // bytes per objective
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
+  const int voff = lane * 16;
+  const double* es = a.excl ? a.excl : a.xpad;               // f64 [*][DIM] (exact equality)
+  const int ne = a.excl ? a.n_excl : a.n_train;
+  double top_v = -__builtin_inf();
+  long long top_i = -1;
+  for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const long long j = tile * kTile + wave * 16 + jl;
+    const bool valid = j < a.n_cand;
+    double c[DIM];
+    load_candidate<DIM>(a, j, valid, c);
+    float c32[DIM];
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) c32[k] = (float)c[k];
+    double acq = 0.0;
+    for (int o = 0; o < a.n_obj; ++o) {
+      const float nl2 = (float)(a.nhl[o] * 1.4426950408889634);
+      const float lpv = (float)log2(a.pv[o]);
+      auto kval = [&](int f) -> float {
+        const float* r = xs + f * DIM;
+        float d2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) { const float d = r[k] - c32[k]; d2 = __builtin_fmaf(d, d, d2); }
+        return __builtin_amdgcn_exp2f(__builtin_fmaf(d2, nl2, lpv));
+      };
+      auto chunk = [&](int ch, float (&B)[16]) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) B[s] = kval(64 * ch + 16 * (s >> 2) + 4 * g + (s & 3));
+      };
+      const float* alo = al + (size_t)o * a.n_pad;
+      const int base = (int)(o * w_obj);
+      f4 w[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = wload32(wr, voff, base + q * 1024);
+      int pos = 0;
+      float mpart = 0.0f, qpart = 0.0f;
+      f4 acc[kC32MaxEp][4];
+      for (int e0 = 0; e0 < nch; e0 += kC32MaxEp) {
+        const int eN = nch - e0 < kC32MaxEp ? nch - e0 : kC32MaxEp;
+#pragma unroll
+        for (int e = 0; e < kC32MaxEp; ++e)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[e][b] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+        const bool mu_on = e0 == 0;
+        auto chunk_step = [&](int ch, const float (&B)[16], float (&Bn)[16]) {
+          const int chn = ch > e0 ? ch - 1 : ch;
+          const int n_here = ch - e0 + 1 < eN ? ch - e0 + 1 : eN;
+          auto ep_body = [&](auto e_c) {
+            constexpr int e = decltype(e_c)::value;
+            if constexpr (e == 0) {
+              if (mu_on) {
+#pragma unroll
+                for (int s = 0; s < 16; ++s)
+                  mpart = __builtin_fmaf(alo[64 * ch + 16 * (s >> 2) + 4 * g + (s & 3)], B[s], mpart);
+              }
+              chunk(chn, Bn);
+            }
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[e][b] = mfma32(w[4 * kq + b][t], B[4 * kq + t], acc[e][b]);
+              const int so = base + (pos + 1) * 16384 + kq * 4096;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) w[4 * kq + b] = wload32(wr, voff, so + b * 1024);
+            }
+            ++pos;
+            if (ch - e0 == e) {
+              mfma_fence32(acc[e][0], acc[e][1], acc[e][2], acc[e][3]);
+#pragma unroll
+              for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) qpart = __builtin_fmaf(B[4 * b + r], acc[e][b][r], qpart);
+            }
+          };
+          EpChain<0, kC32MaxEp>::run(ep_body, n_here);
+        };
+        float BX[16], BY[16];
+        chunk(nch - 1, BX);
+        int ch = nch - 1;
+        for (; ch - 1 >= e0; ch -= 2) {
+          chunk_step(ch, BX, BY);
+          chunk_step(ch - 1, BY, BX);
+        }
+        if (ch >= e0) chunk_step(ch, BX, BY);
+      }
+      qpart += __shfl_xor(qpart, 16, 64);
+      qpart += __shfl_xor(qpart, 32, 64);
+      mpart += __shfl_xor(mpart, 16, 64);
+      mpart += __shfl_xor(mpart, 32, 64);
+      const double pv = a.pv[o], pm = a.pm[o];
+      const double mu = pm + (double)mpart;                               // :486-488
+      const double var = fmax(pv - 2.0 * (double)qpart, BO_MIN_VARIANCE);  // :532-535
+      const double smu = (mu - pm) / a.rsq_pv[o];                         // :563-565
+      const double svar = var / pv;                                       // :568-570
+      const double u = smu + a.beta[o] * sqrt(fabs(svar));                // acquisition.py:52
+      acq = (o == 0) ? u : acq + u;                                       // acquisition.py:108
+      if (valid && g == 0) {
+        const long long off = (long long)o * a.ld_out + j;
+        if (a.mu) a.mu[off] = mu;
+        if (a.var) a.var[off] = var;
+        if (a.std_mu) a.std_mu[off] = smu;
+        if (a.std_var) a.std_var[off] = svar;
+        if (a.ucb) a.ucb[off] = u;
+      }
+    }
+    if (valid && g == 0 && a.acq) a.acq[j] = acq;
+    if (a.topq > 0) {
+      long long gi = valid ? a.cand_offset + j : -1;
+      const double tv = __shfl(top_v, a.topq - 1, 64);
+      const long long ti = __shfl(top_i, a.topq - 1, 64);
+      const bool need = gi >= 0 && bo_better(acq, gi, tv, ti);
+      if (__ballot(need) != 0ull) {
+        // acquisition.py:137-139, exact f64 coordinates; lane group g checks points g, g+4, ...
+        bool hit = false;
+        for (int e = g; e < ne; e += 4) {
+          const double* r = es + (size_t)e * DIM;
+          bool eq = true;
+#pragma unroll
+          for (int k = 0; k < DIM; ++k) eq = eq && (r[k] == c[k]);
+          hit = hit || eq;
+        }
+        const unsigned long long hb = __ballot(hit);
+        if (((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull) gi = -1;
+      }
+      bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+    }
+  }
+  BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
+  if (a.topq > 0 && lane < a.topq) {
+    TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
+    dst[lane].v = top_v;
+    dst[lane].i = top_i;
+  }
+}
+
+__global__ void selftest_mfma32_kernel(const float* a, const float* b, float* d) {
+  const int l = threadIdx.x;
+  const float av = a[(l & 15) * 4 + (l >> 4)];   // A[i=l&15][k=l>>4]
+  const float bv = b[(l >> 4) * 16 + (l & 15)];  // B[k=l>>4][j=l&15]
+  f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  acc = mfma32(av, bv, acc);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) d[(4 * (l >> 4) + r) * 16 + (l & 15)] = acc[r];
+}
+
 inline int pad_rows(long long n) { return (int)((n + 31) / 32 * 32); }
 inline int pad_dim(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : (d <= 6 ? 6 : 8)); }
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1128,6 +1379,7 @@ struct Plan {
   bool sep;              // ... with the integer-grid K* generation
   int off_tbl, off_rw;   // LDS offsets in doubles
   bool rw_cache;          // SEP row factors cached per objective
+  bool fp32;              // cm32_predict_kernel (BO_PREDICT_FP32)
   int grid, waves;       // persistent grid, waves per workgroup
   long long n_tiles;
   size_t lds;
@@ -1150,7 +1402,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
     return BO_ERR_ARG;
   if (d->n_train < 1 || d->n_cand < 0 || d->topq < 0 || d->topq > BO_MAX_TOPQ) return BO_ERR_ARG;
   if (d->cand_kind < 0 || d->cand_kind > 2) return BO_ERR_ARG;
-  if (d->mode & ~(BO_PREDICT_DENSE | BO_PREDICT_NO_SEPARABLE)) return BO_ERR_ARG;
+  if (d->mode & ~(BO_PREDICT_DENSE | BO_PREDICT_NO_SEPARABLE | BO_PREDICT_FP32)) return BO_ERR_ARG;
   if (d->excl_points && d->n_excl < 0) return BO_ERR_ARG;
   const long long n = d->n_train;
   if (n > (1 << 14)) return BO_ERR_UNSUPPORTED;
@@ -1160,10 +1412,20 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   // chunk-major kernel (cm_predict_kernel) for N <= 512; on the reference's 'ij' grid with
   // 16-aligned rows it generates K* from per-row factors and an exp table (pl->sep)
   pl->sep = false;
+  pl->fp32 = false;
   pl->rw_cache = false;
   pl->cm = false;
   pl->off_tbl = pl->off_rw = 0;
-  if (!kmem) {
+  pl->fp32 = (d->mode & BO_PREDICT_FP32) && !kmem;
+  if (pl->fp32) {
+    const int n_pad = (int)((n + 63) / 64 * 64);
+    pl->n_pad = n_pad;
+    pl->ns = 16;
+    pl->multi = false;
+    pl->n_panels = 1;
+    pl->lds = ((size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad) * sizeof(float);
+    if (pl->lds > 160 * 1024) return BO_ERR_UNSUPPORTED;
+  } else if (!kmem) {
     const int n_pad = pad_rows(n);
     const size_t base = (size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad + excl_lds;
     pl->cm = true;
@@ -1188,7 +1450,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
       }
     }
   }
-  if (!pl->cm) {
+  if (!pl->cm && !pl->fp32) {
     int n_pad = pad_rows(n);
     int ns;
     bool multi = false;
@@ -1272,6 +1534,18 @@ hipError_t launch_cm(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
                   : launch_cm_k<DIM, false, true>(fa, pl.grid, pl.lds, st);
   return pl.sep ? launch_cm_k<DIM, true, false>(fa, pl.grid, pl.lds, st)
                 : launch_cm_k<DIM, false, false>(fa, pl.grid, pl.lds, st);
+}
+
+template <int DIM>
+hipError_t launch_c32(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  auto k = cm32_predict_kernel<DIM>;
+  if (pl.lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)pl.lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(pl.grid), dim3(256), pl.lds, st, fa);
+  return hipGetLastError();
 }
 
 hipError_t launch_kmem(const Plan& pl, const FusedArgs& fa, hipStream_t s) {
@@ -1382,7 +1656,10 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   {
     const long long total = (long long)d->n_obj * pl.n_pad * pl.n_pad / 2;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    if (pl.cm)
+    if (pl.fp32)
+      hipLaunchKernelGGL(pack32_kernel, dim3(blocks), dim3(256), 0, s, (f4*)wpack, d->kinv, d->ld_k,
+                         (int)d->n_train, pl.n_pad, d->n_obj);
+    else if (pl.cm)
       hipLaunchKernelGGL(pack_cm_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, fa.upper,
                          (int)d->n_train, pl.n_pad, d->n_obj);
     else
@@ -1416,6 +1693,12 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   const bool timed = g_timer.on && g_timer.used + 2 <= (int)g_timer.ev.size();
   if (timed) timer_mark(s);
   if (kmem) e = launch_kmem(pl, fa, s);
+  else if (pl.fp32) switch (pl.dim_pad) {
+    case 2: e = launch_c32<2>(pl, fa, s); break;
+    case 4: e = launch_c32<4>(pl, fa, s); break;
+    case 6: e = launch_c32<6>(pl, fa, s); break;
+    default: e = launch_c32<8>(pl, fa, s); break;
+  }
   else if (pl.cm) switch (pl.dim_pad) {
     case 2: e = launch_cm<2>(pl, fa, s); break;
     case 4: e = launch_cm<4>(pl, fa, s); break;
@@ -1529,6 +1812,13 @@ int bo_debug_dbgq(double* host) {
   return BO_OK;
 }
 #endif
+
+int bo_selftest_mfma_f32(const float* a, const float* b, float* dd, void* stream) {
+  if (!a || !b || !dd) return BO_ERR_ARG;
+  hipLaunchKernelGGL(selftest_mfma32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, dd);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
 
 int bo_selftest_mfma_f64(const double* a, const double* b, double* dd, void* stream) {
   if (!a || !b || !dd) return BO_ERR_ARG;

@@ -126,7 +126,7 @@ def _fill_desc(x_train, y_train, kinv, cands, pm, pv, ls, betas, offset, count, 
     return d
 
 
-MODES = {"auto": 0, "dense": 1, "auto-exp": 2, "dense-exp": 3}
+MODES = {"auto": 0, "dense": 1, "auto-exp": 2, "dense-exp": 3, "fp32": 4}
 
 
 def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, prior_variance,
@@ -142,7 +142,9 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     q = 2 k^T (U k), U = upper triangle of (K^-1 + K^-T)/2 with the diagonal halved (the same
     form, half the matrix-core work, no factorisation); "dense" is update_variance's
     k^T (K^-1 k) verbatim.  The "-exp" modes disable the integer-grid
-    separable K* generation (exp table) and evaluate every K* entry with exp().
+    separable K* generation (exp table) and evaluate every K* entry with exp().  "fp32" runs
+    K* and the upper-form contraction in f32 on the f32 matrix cores (BASELINE config C5) and
+    everything after the mean / quadratic form in f64.
     """
     dev = require_device(device)
     x_train = as_dev(x_train, dev)

@@ -37,6 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_F64_MATRIX_TFLOPS = 78.6        # MI355X dense FP64 matrix peak (datasheet)
+PEAK_F32_MATRIX_TFLOPS = 157.3       # MI355X dense FP32 matrix peak (datasheet; --mode fp32)
 PEAK_HBM_GBPS = 8000.0
 
 # BASELINE.json configs (SURVEY.md §8 table / §8d synthetic inputs).  C3 is the headline
@@ -66,6 +67,9 @@ def executed_mfma_flops_per_candidate(mode, n=N_TRAIN, n_obj=N_OBJ):
     flops, 16 candidates per wave, nch = padded N / 32 chunks of 32 rows): dense issues
     16 nch^2 MFMAs per 16 candidates and objective, upper the blocks ep <= c only,
     8 nch (nch + 1) (q = 2 k.(U k), U = upper triangle of sym(K^-1))."""
+    if mode == "fp32":   # 16x16x4 f32 MFMAs, 64-row chunks and E-quads: 64 MFMAs per (chunk, E-quad)
+        nch = -(-n // 64)
+        return n_obj * 32 * nch * (nch + 1) * 2048 // 16
     nch = -(-n // 32)
     mfmas = 16 * nch * nch if mode == "dense" else 8 * nch * (nch + 1)
     return n_obj * mfmas * 2048 // 16
@@ -178,8 +182,9 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="C3",
                     help="BASELINE.json config (C3 = the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("auto", "dense"), default="auto",
-                    help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved)")
+    ap.add_argument("--mode", choices=("auto", "dense", "fp32"), default="auto",
+                    help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved); "
+                         "fp32 = the same form on the f32 matrix cores (BASELINE config C5)")
     ap.add_argument("--acq", choices=("sum_ucb", "hvi"), default="sum_ucb",
                     help="sum_ucb = the reference's 'hypervolume improvement' (sum of UCBs, fused top-q); "
                          "hvi = exact hypervolume improvement over the evaluated Pareto front (extension)")
@@ -312,6 +317,7 @@ def main():
                   else f"candidate-points/sec (GP predict + HVI), BASELINE config {args.config}")
         if args.acq == "hvi":
             metric += " [acquisition: exact hypervolume improvement, not the reference's sum of UCBs]"
+        peak = PEAK_F32_MATRIX_TFLOPS if args.mode == "fp32" else PEAK_F64_MATRIX_TFLOPS
         res = {
             "metric": metric,
             "value": total / t_step,
@@ -323,23 +329,25 @@ def main():
             "higher_is_better": True,
             "scaling": cfg["scaling"],
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32" if args.mode == "fp32" else "f64",
             "data": ("synthetic (toy_function on a seeded design)" if cand[0] == "grid" else
                      "synthetic (toy_function_3d on a seeded design drawn from the Sobol set)"),
             "config": {"workload": cfg["workload"], "n_train": n, "n_cand_per_gpu": per_rank,
                        "n_cand_total": total, "n_objectives": n_obj, "dim": d, "topq": q,
                        "parallelism": f"candidate-shard x{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F64_MATRIX_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / PEAK_F64_MATRIX_TFLOPS,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
+                         "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": pmc_traffic() if args.config == "C3" else None,
-                         "kernel": (f"cm_predict_kernel<{2 if d <= 2 else 6}, {'true' if cand[0] == 'grid' else 'false'}, "
+                         "kernel": (f"cm32_predict_kernel<{2 if d <= 2 else 6}>" if args.mode == "fp32" else
+                                    f"cm_predict_kernel<{2 if d <= 2 else 6}, {'true' if cand[0] == 'grid' else 'false'}, "
                                     f"{'true' if args.mode == 'auto' else 'false'}>"),
                          "kernel_ms": k_ms, "flops_per_candidate": f,
                          "formulation": ("upper: q = 2 k.(U k), U = triu((K^-1 + K^-T)/2), diag/2" if args.mode == "auto"
-                                         else "dense: q = k^T (K^-1 k)"),
+                                         else "upper form in f32 (mu, q accumulated in f32, the rest f64)"
+                                         if args.mode == "fp32" else "dense: q = k^T (K^-1 k)"),
                          "executed_mfma_flops_per_candidate": fx,
                          "executed_mfma_tflops": fx * per_rank / (k_ms * 1e-3) / 1e12,
-                         "executed_mfma_frac": fx * per_rank / (k_ms * 1e-3) / 1e12 / PEAK_F64_MATRIX_TFLOPS},
+                         "executed_mfma_frac": fx * per_rank / (k_ms * 1e-3) / 1e12 / peak},
             "selected": [int(i) for i in sel[1]],
         }
         if args.acq == "hvi":

@@ -72,11 +72,15 @@ int bo_device_count(void);
  * disables the integer-grid fast K* generation (K* = pv * R(f) * T[x_last - c_last], an exp
  * table over the last grid axis; used only when the candidates are a grid whose last axis is
  * a multiple of 16 and every training point's last coordinate is an integer on that axis,
- * checked on the device). */
+ * checked on the device).  BO_PREDICT_FP32 (BASELINE config C5, "fp32 with fp64 reference
+ * check"): K* and the upper-form contraction in f32 on v_mfma_f32_16x16x4_f32, the mean and
+ * quadratic form accumulated in f32, everything after them in f64; every candidate evaluates
+ * exp (no grid table); DENSE / NO_SEPARABLE are ignored with it. */
 typedef enum bo_predict_mode {
   BO_PREDICT_AUTO = 0,
   BO_PREDICT_DENSE = 1,
-  BO_PREDICT_NO_SEPARABLE = 2
+  BO_PREDICT_NO_SEPARABLE = 2,
+  BO_PREDICT_FP32 = 4
 } bo_predict_mode;
 
 typedef struct bo_predict_desc {
@@ -237,6 +241,8 @@ int bo_profile_stop(double* total_ms, int* launches);
  * Self test: D[16][16] = A[16][4] * B[4][16] on one f64 MFMA (layout check). Device ptrs.
  * ---------------------------------------------------------------------------------- */
 int bo_selftest_mfma_f64(const double* a16x4, const double* b4x16, double* d16x16, void* stream);
+/* the same on one v_mfma_f32_16x16x4_f32 (the BO_PREDICT_FP32 kernel's layout). Device ptrs. */
+int bo_selftest_mfma_f32(const float* a16x4, const float* b4x16, float* d16x16, void* stream);
 
 #ifdef __cplusplus
 }
