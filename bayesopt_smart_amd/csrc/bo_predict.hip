@@ -732,6 +732,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           auto ep_body = [&](auto e_c) {
             constexpr int e = decltype(e_c)::value;
             (void)B;
+#ifdef BO_ABL_SYNC64
+            __builtin_amdgcn_s_barrier();
+#endif
             if constexpr (e == 0) {
               gen.s0(K, al, mu_on, chn, g, An);
               __builtin_amdgcn_sched_barrier(0);
@@ -1269,11 +1272,16 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
           const int n_here = ch - e0 + 1 < eN ? ch - e0 + 1 : eN;
           auto ep_body = [&](auto e_c) {
             constexpr int e = decltype(e_c)::value;
+            // keep the workgroup's 4 waves on the same E-quad block: they stream identical W
+            // data, so the lockstep turns 3 of 4 L2 reads into L1 hits (C5: W = 8.6 MB per
+            // objective does not fit an XCD's L2; measured 141 -> 108 ms per 2^20 candidates)
+            __builtin_amdgcn_s_barrier();
             if constexpr (e == 0) {
-              if (mu_on) {
+              // branch-free (a join here would drain the W ring with vmcnt(0))
 #pragma unroll
-                for (int s = 0; s < 16; ++s)
-                  mpart = __builtin_fmaf(alo[64 * ch + 16 * (s >> 2) + 4 * g + (s & 3)], B[s], mpart);
+              for (int s = 0; s < 16; ++s) {
+                const float av = alo[64 * ch + 16 * (s >> 2) + 4 * g + (s & 3)];
+                mpart = __builtin_fmaf(mu_on ? av : 0.0f, B[s], mpart);
               }
               chunk(chn, Bn);
             }
