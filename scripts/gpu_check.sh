@@ -25,7 +25,7 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   export TMPDIR=/tmp
   cd /tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- \
-      python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1; rc=$?
+      python "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1; rc=$?
   echo "rocprof rc=$rc"; tail -3 "$R/gpurun_out/prof.log"
   find "$R/gpurun_out/prof" -name "*stats*" | head
 fi
