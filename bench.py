@@ -182,13 +182,16 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="C3",
                     help="BASELINE.json config (C3 = the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("auto", "dense", "fp32"), default="auto",
+    ap.add_argument("--mode", choices=("auto", "dense", "fp32"), default=None,
                     help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved); "
-                         "fp32 = the same form on the f32 matrix cores (BASELINE config C5)")
+                         "fp32 = the same form on the f32 matrix cores; default: fp32 for C5 (BASELINE: "
+                         "'8xMI355X fp32 with fp64 reference check'), auto otherwise")
     ap.add_argument("--acq", choices=("sum_ucb", "hvi"), default="sum_ucb",
                     help="sum_ucb = the reference's 'hypervolume improvement' (sum of UCBs, fused top-q); "
                          "hvi = exact hypervolume improvement over the evaluated Pareto front (extension)")
     args = ap.parse_args()
+    if args.mode is None:
+        args.mode = "fp32" if args.config == "C5" else "auto"
     cfg = CONFIGS[args.config]
 
     import torch
