@@ -20,6 +20,6 @@ print(json.dumps({"lib": os.path.basename(sys.argv[1]), "mode": sys.argv[2], "cf
 '''
 for rnd in range(2):
     for lib in sys.argv[1:]:
-        for mode, cfgname in (("auto", "C3"), ("auto", "C4"), ("fp32", "C5")):
+        for mode, cfgname in [tuple(a.split(":")) for a in os.environ.get("AB_CASES", "auto:C3,auto:C4,fp32:C5").split(",")]:
             r = subprocess.run([sys.executable, "-c", code, lib, mode, cfgname], capture_output=True, text=True)
             print(r.stdout.strip() or r.stderr[-1500:], flush=True)
