@@ -86,6 +86,7 @@ struct FusedArgs {
   long long sep_lo;
   int off_tbl, off_rw;
   int rw_cache;                          // SEP row factors kept for every objective (LDS permitting)
+  int off_sq;                            // > 0: explicit-candidate exponent in dot form (KRows DOTX)
 };
 
 template <int DIM>
@@ -509,8 +510,38 @@ struct EpChain<N, N> {
   static __device__ __forceinline__ void run(F&, int) {}
 };
 
-template <int DIM, bool SEP>
+// 2^t for the non-positive exponents of K* (t = -inf or very negative -> exactly 0): range
+// reduction to r in [-1/2, 1/2], Taylor degree 13 in r ln 2 (|term 14| < 2e-16 relative), no
+// overflow branches (the argument is never positive).
+__device__ __forceinline__ double exp2_nonpos(double t) {
+  const double x = fmax(t, -1100.0);
+  const double n = __builtin_rint(x);
+  const double r = x - n;
+  double p = 1.36914888539041241e-12;
+  p = __builtin_fma(p, r, 2.56784359934881958e-11);
+  p = __builtin_fma(p, r, 4.44553827187081007e-10);
+  p = __builtin_fma(p, r, 7.05491162080112088e-09);
+  p = __builtin_fma(p, r, 1.01780860092396960e-07);
+  p = __builtin_fma(p, r, 1.32154867901443053e-06);
+  p = __builtin_fma(p, r, 1.52527338040598377e-05);
+  p = __builtin_fma(p, r, 1.54035303933816061e-04);
+  p = __builtin_fma(p, r, 1.33335581464284411e-03);
+  p = __builtin_fma(p, r, 9.61812910762847688e-03);
+  p = __builtin_fma(p, r, 5.55041086648215762e-02);
+  p = __builtin_fma(p, r, 2.40226506959100694e-01);
+  p = __builtin_fma(p, r, 6.93147180559945286e-01);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_ldexp(p, (int)n);
+}
+
+// DOTX (explicit candidates, LDS permitting): the exponent of pv exp(nhl |x_f - c|^2) in base 2
+// as nl2 |x_f|^2 + (nl2 |c|^2 + log2 pv) + sum_k x_fk (-2 nl2 c_k), nl2 = nhl log2 e, with
+// |x_f|^2 from LDS and the candidate terms per lane: DIM + 1 FMAs instead of 2 DIM + 2 f64
+// instructions, pv folded into the exponent, and exp2_nonpos instead of exp.
+template <int DIM, bool SEP, bool DOTX = false>
 struct KRows {
+  const double* sq;   // DOTX: [n_pad] |x_f|^2 (inf for padded rows)
+  double cj, nl2, dk[DIM];
   const double* rv;   // SEP: [n_pad] pv * R(f) (0 for padded rows)
   const int* rb;      // SEP: [n_pad] table index base (x_f,last - lo_last) + S - 1; jl = col0 + lane
   const double* tb;   // SEP: objective's table T
@@ -523,6 +554,17 @@ struct KRows {
     return pv * (double)(f + jl);
 #endif
     if (SEP) return rv[f] * tb[rb[f] - jl];
+    if (DOTX) {
+      const d2* r = (const d2*)(xs + f * DIM);
+      double t = __builtin_fma(nl2, sq[f], cj);
+#pragma unroll
+      for (int k = 0; k < DIM / 2; ++k) {
+        const d2 x = r[k];
+        t = __builtin_fma(x.x, dk[2 * k], t);
+        t = __builtin_fma(x.y, dk[2 * k + 1], t);
+      }
+      return exp2_nonpos(t);
+    }
     return pv * exp(sqdist<DIM>(xs, f, c) * nhl);
   }
   // the 8 values of 32-row chunk `ch` this lane feeds to the MFMAs: rows 32 ch + 4 s + g
@@ -538,11 +580,12 @@ struct KRows {
 // of the mean) completes under MFMAs instead of stalling the wave before the chunk:
 //   s0: rv[f], rb[f], alpha[f] loads     s1: table loads T[rb - jl]     s2: the products.
 // The exp path (!SEP) is VALU work that serialises with f64 MFMAs anyway: all of it in s2.
-template <int DIM, bool SEP>
+template <int DIM, bool SEP, bool DOTX = false>
 struct KGen {
+  using KR = KRows<DIM, SEP, DOTX>;
   double rv[8], tv[8];
   int rb[8];
-  __device__ __forceinline__ void s0(const KRows<DIM, SEP>& K, const double* al, bool mu_on, int ch,
+  __device__ __forceinline__ void s0(const KR& K, const double* al, bool mu_on, int ch,
                                      int g, double (&A)[8]) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -553,7 +596,7 @@ struct KGen {
     }
   }
   // s0 without the alpha values (the variance epilogue's regeneration)
-  __device__ __forceinline__ void s0k(const KRows<DIM, SEP>& K, int ch, int g) {
+  __device__ __forceinline__ void s0k(const KR& K, int ch, int g) {
     if (SEP) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
@@ -563,13 +606,13 @@ struct KGen {
       }
     }
   }
-  __device__ __forceinline__ void s1(const KRows<DIM, SEP>& K) {
+  __device__ __forceinline__ void s1(const KR& K) {
     if (SEP) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) tv[s] = K.tb[rb[s] - K.jl];
     }
   }
-  __device__ __forceinline__ void s2(const KRows<DIM, SEP>& K, int ch, int g, double (&B)[8]) {
+  __device__ __forceinline__ void s2(const KR& K, int ch, int g, double (&B)[8]) {
 #ifdef BO_ABL_NOGEN
     K.chunk(ch, g, B);
     return;
@@ -583,7 +626,7 @@ struct KGen {
   }
 };
 
-template <int DIM, bool SEP, bool UPPER>
+template <int DIM, bool SEP, bool UPPER, bool DOTX = false>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   constexpr bool upper = UPPER;
   const double* xs = smem;                                  // [n_pad][DIM]
@@ -687,12 +730,20 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
     double acq = 0.0;
     for (int o = 0; o < a.n_obj; ++o) {
       if (SEP && !a.rw_cache) row_pass(c, o, o + 1);
-      KRows<DIM, SEP> K;
+      KRows<DIM, SEP, DOTX> K;
       K.rv = rv + (a.rw_cache ? (size_t)o * a.n_pad : 0); K.rb = rb; K.tb = tbl + (size_t)o * TS;
       K.xs = xs; K.pv = a.pv[o]; K.nhl = a.nhl[o];
       K.jl = SEP ? col0 + jl : jl;   // T index = rb[f] - (col0 + jl) = x_f,last - c_last + S - 1
 #pragma unroll
       for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
+      if (DOTX) {
+        K.sq = smem + a.off_sq;
+        K.nl2 = a.nhl[o] * 1.4426950408889634;
+        double cc = 0.0;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) { cc = __builtin_fma(c[k], c[k], cc); K.dk[k] = -2.0 * K.nl2 * c[k]; }
+        K.cj = __builtin_fma(K.nl2, cc, log2(a.pv[o]));
+      }
 #ifdef BO_ABL_STAMPS
       STAMP(t_b); st_sum[0] += t_b - t_a; t_a = t_b;   // tile setup + row pass
 #endif
@@ -718,7 +769,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         // sets alternate: no register copies between the chunks).  Branch-free: the last chunk
         // regenerates itself (chn clamped) and groups after the first add 0 x alpha to mu.
         const bool mu_on = e0 == 0;
-        KGen<DIM, SEP> gen;
+        KGen<DIM, SEP, DOTX> gen;
         auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8], const double (&A)[8],
                               double (&An)[8]) {
           // next chunk: ascending (dense) / descending (upper); the last one regenerates itself
@@ -816,7 +867,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         // E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence and multiplied after
         // its FMAs, so the fences' wait states cover the LDS round trips.
         if (!upper) {
-          KGen<DIM, SEP> gq[2];
+          KGen<DIM, SEP, DOTX> gq[2];
           double S[2][8];
           gq[0].s0k(K, e0, g);
           gq[0].s1(K);
@@ -924,8 +975,15 @@ __global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
       tbl[t] = exp(a.nhl[o] * (m * m));
     }
   }
+  if (!GRID && UPPER && a.off_sq > 0)
+    for (int f = tid; f < a.n_pad; f += blockDim.x) {
+      double q = 0.0;
+      for (int k = 0; k < DIM; ++k) q = __builtin_fma(xs[f * DIM + k], xs[f * DIM + k], q);
+      smem[a.off_sq + f] = q;                                   // padded rows: inf
+    }
   __syncthreads();
   if (GRID && sep) cm_tiles<DIM, true, UPPER>(a, smem);
+  else if (!GRID && UPPER && a.off_sq > 0) cm_tiles<DIM, false, UPPER, !GRID && UPPER>(a, smem);
   else cm_tiles<DIM, false, UPPER>(a, smem);
 }
 
@@ -1388,6 +1446,7 @@ struct Plan {
   int off_tbl, off_rw;   // LDS offsets in doubles
   bool rw_cache;          // SEP row factors cached per objective
   bool fp32;              // cm32_predict_kernel (BO_PREDICT_FP32)
+  int off_sq;             // LDS offset (doubles) of |x_f|^2 for the dot-form exponent, 0 = off
   int grid, waves;       // persistent grid, waves per workgroup
   long long n_tiles;
   size_t lds;
@@ -1421,6 +1480,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   // 16-aligned rows it generates K* from per-row factors and an exp table (pl->sep)
   pl->sep = false;
   pl->fp32 = false;
+  pl->off_sq = 0;
   pl->rw_cache = false;
   pl->cm = false;
   pl->off_tbl = pl->off_rw = 0;
@@ -1456,6 +1516,12 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
         pl->off_rw = (int)(base + tbl);
         pl->lds = (pl->rw_cache ? lds_c : lds_1) * sizeof(double);
       }
+    }
+    // explicit candidates, upper form: |x_f|^2 per training row for the dot-form exponent
+    if (d->cand_kind != BO_CAND_GRID && !(d->mode & BO_PREDICT_DENSE) &&
+        (base + n_pad) * sizeof(double) <= 160 * 1024) {
+      pl->off_sq = (int)base;
+      pl->lds = (base + n_pad) * sizeof(double);
     }
   }
   if (!pl->cm && !pl->fp32) {
@@ -1655,6 +1721,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.off_tbl = pl.off_tbl;
   fa.off_rw = pl.off_rw;
   fa.rw_cache = pl.rw_cache ? 1 : 0;
+  fa.off_sq = pl.off_sq;
   if (pl.sep) {
     BO_CHECK_HIP(hipMemsetAsync(sep_flag, 0, sizeof(int), s));
     hipLaunchKernelGGL(sep_check_kernel, dim3((unsigned)((d->n_train + 255) / 256)), dim3(256), 0, s,
