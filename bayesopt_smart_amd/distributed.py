@@ -24,30 +24,48 @@ def shard_range(n, rank, world):
     return offset, count
 
 
-def exchange_topq(top_val, top_idx, q, group=None):
-    """All-gather every rank's local top-q and merge (NaN first, descending, index ties).
+def exchange_topq_rec(rec, q, group=None, out=None):
+    """ONE all_gather of every rank's top-q record block and the merge.
 
-    top_val/top_idx: tensors [q] on the collective's device (HIP for RCCL, CPU for gloo).
-    Returns numpy (values, global indices) of length <= q, identical on every rank.
+    rec: f64 tensor [2q] on the collective's device (HIP for RCCL, CPU for gloo): values in
+    [:q], int64 global indices bit-cast into [q:] (predict_acquire(top_rec=...) writes it in
+    place).  P * q * 16 bytes in total.  Returns numpy (values, global indices), length <= q,
+    identical on every rank: NaN first, then descending value, ties by ascending index.
     """
     world = dist.get_world_size(group)
-    gv = torch.empty(world * q, dtype=top_val.dtype, device=top_val.device)
-    gi = torch.empty(world * q, dtype=top_idx.dtype, device=top_idx.device)
-    dist.all_gather_into_tensor(gv, top_val.contiguous(), group=group)
-    dist.all_gather_into_tensor(gi, top_idx.contiguous(), group=group)
-    return merge_topq(gv.cpu().numpy(), gi.cpu().numpy(), q)
+    g = out if out is not None else torch.empty(world * 2 * q, dtype=rec.dtype, device=rec.device)
+    dist.all_gather_into_tensor(g, rec.contiguous(), group=group)
+    g = g.view(world, 2 * q)
+    vals = g[:, :q].cpu().numpy()
+    idxs = g[:, q:].contiguous().view(torch.int64).cpu().numpy()
+    return merge_topq(vals, idxs, q)
+
+
+def exchange_topq(top_val, top_idx, q, group=None):
+    """exchange_topq_rec for separate value / index tensors [q] (packed into one record block)."""
+    rec = torch.cat([top_val.to(torch.float64), top_idx.to(torch.int64).view(torch.float64)])
+    return exchange_topq_rec(rec, q, group)
 
 
 def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
-                            betas, q, outputs=("acq",), group=None, device=None):
-    """Score this rank's shard of `cands` and return (local results, global top-q)."""
+                            betas, q, outputs=("acq",), group=None, device=None, scorer=None):
+    """Score this rank's shard of `cands` and return (local results, global top-q).
+
+    `scorer` replaces predict_acquire with the same keyword interface (tests drive the
+    partition and the exchange on CPU ranks with the oracle standing in for the device)."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     off, cnt = shard_range(cands.n, rank, world)
-    r = predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
-                        betas, outputs=outputs, topq=q, offset=off, count=cnt, device=device)
+    score = scorer or predict_acquire
+    kw = {} if scorer is not None else {"device": device}
+    if q > 0:
+        dev = torch.device("cpu") if scorer is not None else device
+        kw["top_rec"] = torch.empty(2 * q, dtype=torch.float64,
+                                    device=dev if dev is not None else torch.device("cuda", torch.cuda.current_device()))
+    r = score(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales, betas,
+              outputs=outputs, topq=q, offset=off, count=cnt, **kw)
     if world == 1:
         sel = merge_topq(r["top_val"].cpu().numpy(), r["top_idx"].cpu().numpy(), q)
     else:
-        sel = exchange_topq(r["top_val"], r["top_idx"], q, group)
+        sel = exchange_topq_rec(kw["top_rec"], q, group)
     return r, sel

@@ -131,7 +131,8 @@ MODES = {"auto": 0, "dense": 1, "auto-exp": 2, "dense-exp": 3, "fp32": 4}
 
 def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, prior_variance,
                     length_scales, betas, *, outputs=("mu", "var", "acq"), topq=0,
-                    excl_points=None, offset=0, count=None, out=None, device=None, mode="auto"):
+                    excl_points=None, offset=0, count=None, out=None, device=None, mode="auto",
+                    top_rec=None):
     """Score candidates [offset, offset+count) of `cands`.
 
     x_train [N, d], y_train [N or T, n_obj] (only the first N rows are read), kinv
@@ -145,6 +146,10 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     separable K* generation (exp table) and evaluate every K* entry with exp().  "fp32" runs
     K* and the upper-form contraction in f32 on the f32 matrix cores (BASELINE config C5) and
     everything after the mean / quadratic form in f64.
+
+    ``top_rec`` (optional f64 device tensor [2 topq]): the selection is written into it as one
+    16-B-per-entry record block -- values in [:topq], int64 indices (bit pattern) in [topq:] --
+    so that the multi-GPU exchange is ONE all_gather of it (distributed.exchange_topq_rec).
     """
     dev = require_device(device)
     x_train = as_dev(x_train, dev)
@@ -186,8 +191,15 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
         desc.acq = res["acq"].data_ptr()
     desc.ld_out = ld_out or count
     if topq:
-        res["top_val"] = torch.empty(topq, dtype=F64, device=dev)
-        res["top_idx"] = torch.empty(topq, dtype=torch.int64, device=dev)
+        if top_rec is not None:
+            if top_rec.dtype != F64 or top_rec.numel() != 2 * topq or not top_rec.is_contiguous() \
+                    or top_rec.device != dev:
+                raise ValueError("top_rec must be a contiguous f64 device tensor of 2 * topq entries")
+            res["top_val"] = top_rec[:topq]
+            res["top_idx"] = top_rec[topq:].view(torch.int64)
+        else:
+            res["top_val"] = torch.empty(topq, dtype=F64, device=dev)
+            res["top_idx"] = torch.empty(topq, dtype=torch.int64, device=dev)
         desc.top_val = res["top_val"].data_ptr()
         desc.top_idx = res["top_idx"].data_ptr()
     lib = _lib.load()

@@ -16,10 +16,21 @@ fused predict/acquisition kernel writing mu, var and acq for every candidate, th
 merge) + the global top-q exchange + the indices on the host.  Inputs (X, y, K^-1) are
 resident in HBM before the timed region.
 
-Prints ONE JSON line (rank 0).  `roofline` is the fused kernel's f64 matrix-core throughput
-(algorithmic flops F per candidate, SURVEY.md §8d) over its HIP-event-timed launches;
-`cpu_baseline` times the C/OpenMP restatement of the reference algorithm (oracle/cpu_ref.c)
-on a bounded slice of the same workload on this host's cores.
+Prints ONE JSON line (rank 0).  `roofline` is the fused kernel's matrix-core throughput over
+its HIP-event-timed launches: `achieved` counts the MFMA flops the kernel executes per candidate
+(the upper form q = 2 k.(U k) issues about half of SURVEY.md §8d's reference-formulation F), so
+`frac` <= 1 is a true fraction of the datasheet peak; the reference-formulation equivalent is
+reported separately as `ref_flop_equiv_tflops`.  `traffic` is the PMC-counted HBM bytes per
+launch and `traffic_ratio` its ratio to the algorithmic bytes.  `cpu_baseline` times the
+C/OpenMP restatement of the reference algorithm (oracle/cpu_ref.c, DGEMM on numpy's OpenBLAS)
+on this process's CPU share; its acquisition array also checks the GPU's selection
+(`selection_matches_cpu`, tie-aware as SURVEY.md §8c) and every acquisition value.
+
+    python bench.py --fit [--config C3|C4|C5]
+
+times the GP fit on the device instead: update_k + invert_k, one
+compute_mll evaluation, and one full Powell hyper-parameter fit (optimize_hyperparams_mll),
+at the config's N_train.
 """
 
 from __future__ import annotations
@@ -135,7 +146,65 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, budget_s=12.0, chunk=16384,
+def host_cpu_share():
+    """(threads to use, description) -- this process's CPU share on the GPU box: the pool's
+    per-GPU share as the host exports it (OMP_NUM_THREADS), else the cgroup quota, else the
+    affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+            if q != "max":
+                quota = max(1, int(float(q) / float(per)))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    threads = int(env) if env and env.isdigit() and int(env) > 0 else (min(aff, quota) if quota else aff)
+    threads = min(threads, aff)
+    phys = None
+    try:
+        cores = set()
+        with open("/proc/cpuinfo") as fh:
+            pid = cid = None
+            for line in fh:
+                if line.startswith("physical id"):
+                    pid = line.split(":")[1].strip()
+                elif line.startswith("core id"):
+                    cid = line.split(":")[1].strip()
+                    cores.add((pid, cid))
+        phys = len(cores) or None
+    except OSError:
+        pass
+    desc = (f"{threads} threads = this process's CPU share (OMP_NUM_THREADS={env}, cgroup quota "
+            f"{quota}, affinity {aff} logical CPUs; machine: {os.cpu_count()} logical / {phys} physical "
+            f"cores, {_cpu_model()})")
+    return threads, desc
+
+
+def selection_check(sel_idx, cpu_acq, excluded, q):
+    """The GPU's global top-q against the CPU reference's acquisition array, with SURVEY.md
+    §8c's tie rule: index equality where the reference's gaps exceed 10x the tolerance, else
+    the reference acq at the chosen index must equal the reference's own rank value."""
+    a = np.where(excluded, -np.inf, np.asarray(cpu_acq, dtype=np.float64))
+    sel = np.asarray(sel_idx, dtype=np.int64)
+    sel = sel[sel >= 0]
+    n_avail = int((~excluded).sum())
+    if sel.size != min(q, n_avail) or excluded[sel].any():
+        return False
+    order = np.argsort(-a, kind="stable")[: q + 1]
+    top = a[order]
+    tol = 1e-5 * np.maximum(1.0, np.abs(top))
+    for t in range(sel.size):
+        gap = t + 1 < top.size and top[t] - top[t + 1] > 10 * tol[t] and (t == 0 or top[t - 1] - top[t] > 10 * tol[t])
+        if gap and sel[t] != order[t]:
+            return False
+        if not gap and abs(a[sel[t]] - top[t]) > 2 * tol[t]:
+            return False
+    return True
+
+
+def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, budget_s=20.0, chunk=32768,
                  max_cand=SIDE * SIDE):
     """Reference algorithm on the host cores: oracle/cpu_ref.c, the C/OpenMP restatement of
     update_k_star -> update_mean -> update_variance (materialised K* per candidate block,
@@ -143,21 +212,24 @@ def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, budget_s=12.0,
     select_next_batch's full descending sort + exclusion walk.
     points(lo, hi) -> f64 [hi - lo, d] candidates of the workload."""
     from oracle import cpu_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads, share = host_cpu_share()
     cpu_ref.load()
     done = 0
     acqs = []
     t0 = time.perf_counter()
     while done < max_cand and time.perf_counter() - t0 < budget_s:
-        acqs.append(cpu_ref.predict_acquire(x, y, points(done, done + chunk), kinv, pm, pv, ls, betas,
+        hi = min(done + chunk, max_cand)
+        acqs.append(cpu_ref.predict_acquire(x, y, points(done, hi), kinv, pm, pv, ls, betas,
                                             threads=threads, outputs=True)["acq"])
-        done += chunk
-    cpu_ref.select(np.concatenate(acqs), points(0, done), x, q)
+        done = hi
+    acq = np.concatenate(acqs)
+    cpu_sel = cpu_ref.select(acq, points(0, done), x, q)
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "candidate-points/sec", "cores": threads, "kind": "port",
-            "sample": f"first {done} candidates of the {label} (N_train={x.shape[0]}, {len(pm)} "
-                      f"objectives, mu/var/acq written, top-{q} select), oracle/cpu_ref.c (C/OpenMP, "
-                      f"{threads} threads of {os.cpu_count()} logical CPUs, {_cpu_model()}), {dt:.1f} s"}
+    res = {"value": done / dt, "unit": "candidate-points/sec", "cores": threads, "kind": "port",
+           "sample": f"{'all' if done == max_cand else 'first'} {done} candidates of the {label} "
+                     f"(N_train={x.shape[0]}, {len(pm)} objectives, mu/var/acq written, top-{q} select), "
+                     f"oracle/cpu_ref.c (C/OpenMP, DGEMM: {cpu_ref.dgemm_name()}), {share}, {dt:.1f} s"}
+    return res, acq, cpu_sel
 
 
 def pmc_traffic():
@@ -174,6 +246,62 @@ def pmc_traffic():
     return None
 
 
+def run_fit(cfg, label, dev):
+    """--fit: the GP fit on the device at the config's N_train.
+    update_k + invert_k (numba_kernels.py:329-403), one compute_mll (:152-235), one Powell fit
+    (optimize_hyperparams_mll, :238-321: every MLL evaluation one device call).  Each timing is
+    the median of repeated calls, synchronised; parity against numpy/LAPACK is reported beside."""
+    import torch
+    import bayesopt_smart_amd as bo
+    from oracle import oracle_np as O
+    x, y, pm, pv, ls, betas, kinv_ref, _ = make_config_problem(cfg, 1)
+    n, n_obj = x.shape[0], len(pm)
+    xd = torch.tensor(x, device=dev)
+    yd = torch.tensor(y, device=dev)
+    km = torch.zeros((n_obj, n, n), dtype=torch.float64, device=dev)
+
+    def timed(fn, reps):
+        ts, out = [], None
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3, out
+
+    def gram_inverse():
+        bo.kernels.update_k(km, xd, 0, n, pv, ls)
+        return bo.kernels.invert_k(n, km)
+
+    gram_inverse()
+    inv_ms, kinv = timed(gram_inverse, 5)
+    kinv = kinv.cpu().numpy()
+    inv_err = float(np.abs(kinv - kinv_ref).max() / np.abs(kinv_ref).max())
+    mll_fn = lambda: bo.kernels.compute_mll(xd, yd, km, pm, pv, ls, n)  # noqa: E731
+    mll_fn()
+    mll_ms, mll = timed(mll_fn, 10)
+    km_h = np.zeros((n_obj, n, n))
+    mll_ref = O.compute_mll(x, y, km_h, pm, pv, ls, n)
+    ls_fit, pv_fit = ls.copy(), pv.copy()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = bo.kernels.optimize_hyperparams_mll(xd, yd, km, pm, pv_fit, ls_fit, n)
+    torch.cuda.synchronize()
+    fit_ms = (time.perf_counter() - t0) * 1e3
+    return {
+        "metric": f"GP fit on device (Gram + inverse, MLL evaluation, Powell fit), {label}",
+        "value": fit_ms, "unit": "ms per Powell hyper-parameter fit", "higher_is_better": False,
+        "n_gpus": 1, "dtype": "f64", "data": "synthetic (the bench workload's training set)",
+        "config": {"workload": cfg["workload"], "n_train": n, "n_objectives": n_obj, "dim": x.shape[1]},
+        "update_k_invert_k_ms": inv_ms, "invert_k_rel_err_vs_lapack": inv_err,
+        "compute_mll_ms": mll_ms, "mll": mll, "mll_lapack": mll_ref,
+        "mll_rel_err": abs(mll - mll_ref) / max(1.0, abs(mll_ref)),
+        "powell_nfev": int(res.nfev), "powell_ms_per_eval": fit_ms / max(int(res.nfev), 1),
+        "fitted_length_scales": ls_fit.tolist(),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -182,6 +310,7 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="C3",
                     help="BASELINE.json config (C3 = the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fit", action="store_true", help="time the device GP fit instead (SURVEY §8f)")
     ap.add_argument("--mode", choices=("auto", "dense", "fp32"), default=None,
                     help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved); "
                          "fp32 = the same form on the f32 matrix cores; default: fp32 for C5 (BASELINE: "
@@ -204,10 +333,16 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.fit:
+        if world > 1:
+            raise SystemExit("--fit is a single-GPU measurement")
+        print(json.dumps(run_fit(cfg, args.config, dev)), flush=True)
+        return
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
     import bayesopt_smart_amd as bo
+    from bayesopt_smart_amd.distributed import shard_range
     lib = bo._lib.load()
 
     x, y, pm, pv, ls, betas, kinv, cand = make_config_problem(cfg, world)
@@ -218,11 +353,12 @@ def main():
         cands = bo.CandidateSet.grid([(0, cand[1]), (0, side)])
         per_rank = side * side
         offset = rank * per_rank
+        total = world * per_rank
     else:
-        # strong scaling: the fixed Sobol set split into P contiguous index ranges
+        # strong scaling: the fixed Sobol set split into P balanced contiguous index ranges
         m = cand[1].shape[0]
-        per_rank = m // world
-        offset = rank * per_rank
+        offset, per_rank = shard_range(m, rank, world)
+        total = m
         cands = bo.CandidateSet.explicit(cand[1], device=dev)
     xd = torch.tensor(x, device=dev)
     yd = torch.tensor(y, device=dev)
@@ -230,8 +366,10 @@ def main():
     outputs = ("mu", "var", "ucb", "acq") if args.config == "C2" or args.acq == "hvi" else ("mu", "var", "acq")
     out = {k: torch.empty((per_rank,) if k == "acq" else (n_obj, per_rank), dtype=torch.float64,
                           device=dev) for k in outputs}
-    gath_v = torch.empty(world * q, dtype=torch.float64, device=dev)
-    gath_i = torch.empty(world * q, dtype=torch.int64, device=dev)
+    # the top-q exchange: each rank's list as ONE block of 16-B records (values, int64 indices),
+    # one all_gather of P * q * 16 bytes
+    rec = torch.empty(2 * q, dtype=torch.float64, device=dev)
+    gath = torch.empty(world * 2 * q, dtype=torch.float64, device=dev)
 
     hvi_ev = []
     if args.acq == "hvi":
@@ -242,8 +380,6 @@ def main():
         ref_pt = y.min(axis=0) - 1.0
         front_y = y[bo.is_pareto_efficient(y)]
         exd = torch.tensor(x, device=dev)
-        tv = torch.empty(q, dtype=torch.float64, device=dev)
-        ti = torch.empty(q, dtype=torch.int64, device=dev)
         sel_ws = torch.empty(lib.bo_select_topq_workspace_size(per_rank, q), dtype=torch.uint8, device=dev)
         glo = (ctypes.c_int64 * 8)(*((list(cands.lo) if cands.lo else []) + [0] * (8 - len(cands.lo or []))))
         gsh = (ctypes.c_int64 * 8)(*((list(cands.shape) if cands.shape else []) + [1] * (8 - len(cands.shape or []))))
@@ -267,24 +403,23 @@ def main():
             bo._lib.check(lib.bo_select_topq(
                 out["acq"].data_ptr(), per_rank, cands.kind_code,
                 cands.tensor[offset:].data_ptr() if cands.tensor is not None else None, glo, gsh,
-                cands.dim, offset, exd.data_ptr(), exd.shape[0], q, tv.data_ptr(), ti.data_ptr(),
-                sel_ws.data_ptr(), sel_ws.numel(), strm), "select")
-            return {"top_val": tv, "top_idx": ti}
+                cands.dim, offset, exd.data_ptr(), exd.shape[0], q, rec.data_ptr(),
+                rec.data_ptr() + 8 * q, sel_ws.data_ptr(), sel_ws.numel(), strm), "select")
 
     def step():
         if args.acq == "hvi":
-            r = step_hvi()
+            step_hvi()
         else:
-            r = bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=outputs,
-                                   topq=q, offset=offset, count=per_rank, out=out, device=dev,
-                                   mode=args.mode)
+            bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=outputs, topq=q,
+                               offset=offset, count=per_rank, out=out, device=dev, mode=args.mode,
+                               top_rec=rec)
         if world > 1:
-            dist.all_gather_into_tensor(gath_v, r["top_val"])
-            dist.all_gather_into_tensor(gath_i, r["top_idx"])
-            v, i = gath_v.cpu().numpy(), gath_i.cpu().numpy()
+            dist.all_gather_into_tensor(gath, rec)
+            g = gath.view(world, 2 * q)
         else:
-            v, i = r["top_val"].cpu().numpy(), r["top_idx"].cpu().numpy()
-        return bo.merge_topq(v, i, q)
+            g = rec.view(1, 2 * q)
+        g = g.cpu()
+        return bo.merge_topq(g[:, :q].numpy(), g[:, q:].contiguous().view(torch.int64).numpy(), q)
 
     for _ in range(args.warmup):
         step()
@@ -314,13 +449,17 @@ def main():
         n, d = cfg["n_train"], cfg["dim"]
         f = flops_per_candidate(n, n_obj, d)
         fx = executed_mfma_flops_per_candidate(args.mode, n, n_obj)
-        achieved = f * per_rank / (k_ms * 1e-3) / 1e12
-        total = world * per_rank
+        executed = fx * per_rank / (k_ms * 1e-3) / 1e12
+        ref_equiv = f * per_rank / (k_ms * 1e-3) / 1e12
         metric = ("candidate-points/sec (GP predict + HVI) at N_train=512, N_cand=1M" if args.config == "C3"
                   else f"candidate-points/sec (GP predict + HVI), BASELINE config {args.config}")
         if args.acq == "hvi":
             metric += " [acquisition: exact hypervolume improvement, not the reference's sum of UCBs]"
         peak = PEAK_F32_MATRIX_TFLOPS if args.mode == "fp32" else PEAK_F64_MATRIX_TFLOPS
+        # algorithmic HBM bytes per candidate: outputs written (+ explicit coordinates read)
+        n_out = sum(1 if k == "acq" else n_obj for k in outputs)
+        alg_bytes = (8 * n_out + (0 if cand[0] == "grid" else 8 * d)) * per_rank
+        traffic = pmc_traffic() if args.config == "C3" and args.mode == "auto" and args.acq == "sum_ucb" else None
         res = {
             "metric": metric,
             "value": total / t_step,
@@ -338,19 +477,23 @@ def main():
             "config": {"workload": cfg["workload"], "n_train": n, "n_cand_per_gpu": per_rank,
                        "n_cand_total": total, "n_objectives": n_obj, "dim": d, "topq": q,
                        "parallelism": f"candidate-shard x{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak,
-                         "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": pmc_traffic() if args.config == "C3" else None,
+            "roofline": {"bound": "mfma", "achieved": executed, "peak": peak, "unit": "TFLOP/s",
+                         "frac": executed / peak,
+                         "flops_basis": f"executed MFMA flops per candidate ({fx}; "
+                                        f"{'upper form' if args.mode != 'dense' else 'dense form'})",
+                         "traffic": traffic,
+                         "algorithmic_bytes": alg_bytes,
+                         "traffic_ratio": (traffic / alg_bytes) if traffic else None,
                          "kernel": (f"cm32_predict_kernel<{2 if d <= 2 else 6}>" if args.mode == "fp32" else
                                     f"cm_predict_kernel<{2 if d <= 2 else 6}, {'true' if cand[0] == 'grid' else 'false'}, "
                                     f"{'true' if args.mode == 'auto' else 'false'}>"),
-                         "kernel_ms": k_ms, "flops_per_candidate": f,
+                         "kernel_ms": k_ms,
                          "formulation": ("upper: q = 2 k.(U k), U = triu((K^-1 + K^-T)/2), diag/2" if args.mode == "auto"
                                          else "upper form in f32 (mu, q accumulated in f32, the rest f64)"
                                          if args.mode == "fp32" else "dense: q = k^T (K^-1 k)"),
                          "executed_mfma_flops_per_candidate": fx,
-                         "executed_mfma_tflops": fx * per_rank / (k_ms * 1e-3) / 1e12,
-                         "executed_mfma_frac": fx * per_rank / (k_ms * 1e-3) / 1e12 / peak},
+                         "ref_flops_per_candidate": f,
+                         "ref_flop_equiv_tflops": ref_equiv},
             "selected": [int(i) for i in sel[1]],
         }
         if args.acq == "hvi":
@@ -373,11 +516,33 @@ def main():
                 def points(lo, hi):
                     return cand[1][lo:hi]
                 label = f"{args.config} Sobol set"
-            res["cpu_baseline"] = cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q,
-                                               max_cand=per_rank)
+            cb, cpu_acq, cpu_sel = cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q,
+                                                max_cand=per_rank)
+            res["cpu_baseline"] = cb
+            # parity of the timed run's own outputs against the CPU reference (outside the timing)
+            done = cpu_acq.size
+            gpu_acq = out["acq"][:done].cpu().numpy()
+            res["acq_max_err_vs_cpu"] = float(np.max(np.abs(gpu_acq - cpu_acq) / np.maximum(1.0, np.abs(cpu_acq))))
+            if done == per_rank:
+                xs = {tuple(r) for r in x}
+                pts = points(0, done)
+                excluded = np.fromiter((tuple(p) in xs for p in pts), dtype=bool, count=done) \
+                    if cand[0] != "grid" else _grid_excluded(x, side, done)
+                res["selection_matches_cpu"] = selection_check(sel[1], cpu_acq, excluded, q)
+                res["cpu_selected"] = [int(i) for i in cpu_sel]
+            else:
+                res["selection_matches_cpu"] = None   # sample shorter than the shard
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _grid_excluded(x, side, m):
+    """Evaluated grid points as a mask over the 'ij' grid's linear index."""
+    ex = np.zeros(m, dtype=bool)
+    lin = x[:, 0].astype(np.int64) * side + x[:, 1].astype(np.int64)
+    ex[lin[(lin >= 0) & (lin < m)]] = True
+    return ex
 
 
 if __name__ == "__main__":

@@ -26,10 +26,20 @@
 
 typedef double v4d __attribute__((vector_size(32)));
 
+/* System DGEMM (cblas_dgemm with 64-bit integers: numpy's bundled OpenBLAS, the BLAS the
+ * reference's np.dot / Numba would call), installed by oracle/cpu_ref.py; NULL -> the built-in
+ * AVX2 register-tiled loop below. */
+typedef void (*dgemm_fn)(int order, int ta, int tb, long m, long n, long k, double alpha,
+                         const double* a, long lda, const double* b, long ldb, double beta,
+                         double* c, long ldc);
+static dgemm_fn g_dgemm = 0;
+void bo_cpu_set_dgemm(void* fn) { g_dgemm = (dgemm_fn)fn; }
+int bo_cpu_has_dgemm(void) { return g_dgemm != 0; }
+
 static void block(int n, int d, int n_obj, const double* x, const double* cand, long i0, int cb,
                   const double* kinv, const double* alpha, const double* pm, const double* pv,
                   const double* ls, const double* beta, double* ks, double* z, double* mu,
-                  double* var, double* acq, long m_stride) {
+                  double* var, double* ucb, double* acq, long m_stride) {
   double acc_b[CB];
   for (int i = 0; i < cb; ++i) acc_b[i] = 0.0;
   for (int o = 0; o < n_obj; ++o) {
@@ -51,6 +61,9 @@ static void block(int n, int d, int n_obj, const double* x, const double* cand, 
     /* Z = K^-1 K* (the reference's DGEMM): 8-candidate strips (a 32 KiB K* strip stays in
      * L1) x 6-row register tiles of K^-1 (12 AVX2 accumulators) */
     const double* w = kinv + (long)o * n * n;
+    if (g_dgemm) /* row-major Z[n][CB] = K^-1[n][n] . K*[n][CB] */
+      g_dgemm(101, 111, 111, n, cb, n, 1.0, w, n, ks, CB, 0.0, z, CB);
+    else
     for (int i0 = 0; i0 < CB; i0 += 8) {
       int e = 0;
       for (; e + 6 <= n; e += 6) {
@@ -94,18 +107,19 @@ static void block(int n, int d, int n_obj, const double* x, const double* cand, 
       if (var) var[(long)o * m_stride + i0 + i] = v;
       const double smu = (muv - pm[o]) / rpv, svar = v / pv[o];
       const double u = smu + beta[o] * sqrt(fabs(svar));
+      if (ucb) ucb[(long)o * m_stride + i0 + i] = u;
       acc_b[i] = (o == 0) ? u : acc_b[i] + u;
     }
   }
   for (int i = 0; i < cb; ++i) acq[i0 + i] = acc_b[i];
 }
 
-/* Scores candidates [0, m) (f64 [m][d]); mu/var [n_obj][m] optional, acq [m] required.
+/* Scores candidates [0, m) (f64 [m][d]); mu/var/ucb [n_obj][m] optional, acq [m] required.
  * kinv [n_obj][n][n]; y [n][n_obj].  Returns 0. */
 int bo_cpu_predict_acquire(int n, int d, int n_obj, const double* x, const double* y,
                            const double* cand, long m, const double* kinv, const double* pm,
                            const double* pv, const double* ls, const double* beta, double* mu,
-                           double* var, double* acq, int threads) {
+                           double* var, double* ucb, double* acq, int threads) {
   double* alpha = (double*)malloc(sizeof(double) * n_obj * n);
   for (int o = 0; o < n_obj; ++o)
     for (int e = 0; e < n; ++e) {
@@ -122,7 +136,7 @@ int bo_cpu_predict_acquire(int n, int d, int n_obj, const double* x, const doubl
     for (long b = 0; b < nblk; ++b) {
       const long i0 = b * CB;
       const int cb = (int)(m - i0 < CB ? m - i0 : CB);
-      block(n, d, n_obj, x, cand, i0, cb, kinv, alpha, pm, pv, ls, beta, ks, z, mu, var, acq, m);
+      block(n, d, n_obj, x, cand, i0, cb, kinv, alpha, pm, pv, ls, beta, ks, z, mu, var, ucb, acq, m);
     }
     free(ks);
     free(z);

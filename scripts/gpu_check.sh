@@ -21,6 +21,22 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
   STEP_OK $rc || exit $rc
 fi
+if [ "$MODE" = all ] || [ "$MODE" = fit ]; then
+  : > gpurun_out/fit.jsonl
+  for c in C3 C4 C5; do
+    timeout -k 10 300 python bench.py --fit --config $c >> gpurun_out/fit.jsonl 2> gpurun_out/fit_$c.err; rc=$?
+    echo "fit $c rc=$rc"; tail -c 600 gpurun_out/fit.jsonl; echo
+    STEP_OK $rc || exit $rc
+  done
+fi
+if [ "$MODE" = configs ]; then
+  : > gpurun_out/configs.jsonl
+  for c in C2 C3 C4 C5; do
+    timeout -k 10 300 python bench.py --config $c >> gpurun_out/configs.jsonl 2> gpurun_out/cfg_$c.err; rc=$?
+    echo "config $c rc=$rc"
+    STEP_OK $rc || exit $rc
+  done
+fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   export TMPDIR=/tmp
   cd /tmp

@@ -81,3 +81,73 @@ def test_shard_range_partitions():
             for (o, c), (o2, _) in zip(spans, spans[1:]):
                 assert o + c == o2
             assert sum(c for _, c in spans) == n
+
+
+def _oracle_scorer(x, y, kinv, cands, pm, pv, ls, betas, *, outputs, topq, offset, count, top_rec):
+    """predict_acquire's keyword interface on the CPU oracle (the device scorer's stand-in):
+    scores candidates [offset, offset + count) and writes the local top-q record block."""
+    from oracle import oracle_np as O
+    pts = cands.points(np.arange(offset, offset + count))
+    ref = O.predict_acquire(x, y, pts, pm, pv, ls, betas, kinv=kinv)
+    xs = {tuple(r) for r in np.asarray(x, dtype=np.float64)}
+    excl = np.array([tuple(p) in xs for p in pts.astype(np.float64)], dtype=bool)
+    loc = O.select_next_batch_indices(ref["acq"], excl, topq)
+    top_rec[:] = 0.0
+    top_rec[:topq] = -np.inf
+    top_rec[topq:].view(torch.int64)[:] = -1
+    top_rec[:loc.size] = torch.as_tensor(ref["acq"][loc])
+    top_rec[topq:topq + loc.size].view(torch.int64)[:] = torch.as_tensor(loc + offset)
+    return {"acq": ref["acq"], "top_val": top_rec[:topq], "top_idx": top_rec[topq:].view(torch.int64)}
+
+
+def _problem(seed):
+    from oracle import oracle_np as O
+    rng = np.random.default_rng(seed)
+    side = 37                                          # 1369 candidates: uneven shards
+    lin = rng.choice(side * side, size=24, replace=False)
+    x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+    y = np.stack([-((x[:, 0] - 15) ** 2) + 100, -((x[:, 1] - 20) ** 2) + 20], axis=1)
+    pm, pv = y.mean(0), y.var(0)
+    ls, betas = np.array([5.0, 7.0]), np.array([2.0, 1.5])
+    km = np.zeros((2, 24, 24))
+    O.update_k(km, x, 0, 24, pv, ls)
+    return side, x, y, pm, pv, ls, betas, O.invert_k(24, km)
+
+
+def _sharded_worker(rank, world, port, q, seed, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bayesopt_smart_amd.distributed import sharded_predict_acquire
+        from bayesopt_smart_amd.predict import CandidateSet
+        side, x, y, pm, pv, ls, betas, kinv = _problem(seed)
+        cands = CandidateSet.grid([(0, side), (0, side)])
+        r, (gv, gi) = sharded_predict_acquire(x, y, kinv, cands, pm, pv, ls, betas, q,
+                                              scorer=_oracle_scorer)
+        out[rank] = (gi.tolist(), r["acq"].size)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,q", [(2, 3), (3, 16)])
+def test_gloo_sharded_predict_acquire_partition_and_exchange(world, q):
+    """sharded_predict_acquire's own partition (shard_range) and its ONE all_gather of packed
+    16-B top-q records, with the CPU oracle scoring each rank's shard, select exactly what the
+    reference's select_next_batch picks over the whole grid (acquisition.py:116-144)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import oracle_np as O
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_worker, args=(world, _free_port(), q, 11, out), nprocs=world, join=True)
+    side, x, y, pm, pv, ls, betas, kinv = _problem(11)
+    grid = O.grid_points([(0, side), (0, side)])
+    ref = O.predict_acquire(x, y, grid, pm, pv, ls, betas, kinv=kinv)
+    xs = {tuple(r) for r in x}
+    excl = np.array([tuple(p) in xs for p in grid.astype(np.float64)])
+    want = O.select_next_batch_indices(ref["acq"], excl, q).tolist()
+    assert sum(out[r][1] for r in range(world)) == side * side
+    for r in range(world):
+        assert out[r][0] == want
+    np.testing.assert_array_equal(grid[want], O.select_next_batch(grid, ref["acq"], x, q))

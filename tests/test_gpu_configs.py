@@ -4,16 +4,17 @@ C1 is the CPU plumbing demo (tests/test_gpu_api.py covers its trajectory) and C3
 workload (tests/test_gpu_predict.py::test_full_size_c3_properties).  Inputs follow SURVEY.md
 §8d: seeded designs, the reference's objectives (examples/benchmark_functions.py:33-73), prior
 statistics from the samples, unscrambled Sobol candidates scaled to [0, 300)^6 for the 6-D
-configs.  Parity is checked against the CPU oracle (the reference algorithm) on a candidate
-subsample with the SURVEY.md §8c tolerances, and on the full candidate sets through
-size-independent properties: top-q consistent with the acquisition array, shard merge equal
-to the single call."""
+configs.  Parity is checked on EVERY candidate against oracle/cpu_ref.c (the reference
+algorithm on the host cores, tests/fullref.py) with the SURVEY.md §8c tolerances, the top-q
+selection is judged against the CPU acquisition array, and the shard merge must equal the
+single call."""
 
 import numpy as np
 import pytest
 
 from oracle import oracle_np as O
 from parity import check_predict, check_topq
+from fullref import cpu_full, grid_points_2d
 
 pytestmark = pytest.mark.gpu
 
@@ -78,13 +79,12 @@ def test_c2_grid_ucb(bo, mode):
     d = problem(x, toy_function(x), 20.0, 2.0)
     cands = bo.predict.CandidateSet.grid([(0, side), (0, side)])
     out = run(bo, d, cands, 3, mode, outputs=("mu", "var", "ucb", "acq"))
-    sub = np.sort(rng.choice(side * side, size=8192, replace=False))
-    ref = O.predict_acquire(x, d["y"], cands.points(sub), d["pm"], d["pv"], d["ls"], d["betas"],
-                            kinv=d["Kinv"])
-    check_predict({k: out[k][..., sub] for k in ("mu", "var", "ucb", "acq")}, ref, d["pv"])
+    ref = cpu_full("C2", x, d["y"], grid_points_2d(side, side), d["Kinv"], d["pm"], d["pv"], d["ls"],
+                   d["betas"])
+    check_predict({k: out[k] for k in ("mu", "var", "ucb", "acq")}, ref, d["pv"])
     excl = np.zeros(side * side, dtype=bool)
     excl[lin] = True
-    check_topq(out["top_idx"], out["acq"], excl, 3)
+    check_topq(out["top_idx"], ref["acq"], excl, 3)
 
 
 @pytest.mark.parametrize("mode", ["auto", "dense"])
@@ -99,11 +99,10 @@ def test_c4_c5_sobol_6d_3obj(bo, n, m_full, q, mode):
     d = problem(x, toy_function_3d(x), 40.0, 2.0)
     cands = bo.predict.CandidateSet.explicit(cand)
     out = run(bo, d, cands, q, mode)
-    sub = np.sort(rng.choice(m_full, size=4096, replace=False))
-    ref = O.predict_acquire(x, d["y"], cand[sub], d["pm"], d["pv"], d["ls"], d["betas"], kinv=d["Kinv"])
-    check_predict({k: out[k][..., sub] for k in ("mu", "var", "acq")}, ref, d["pv"])
+    ref = cpu_full(("C45", n, m_full), x, d["y"], cand, d["Kinv"], d["pm"], d["pv"], d["ls"], d["betas"])
+    check_predict({k: out[k] for k in ("mu", "var", "acq")}, ref, d["pv"])
     # every training point is drawn from the candidate set: all of them are excluded
-    check_topq(out["top_idx"], out["acq"], excluded_rows(cand, x), q)
+    check_topq(out["top_idx"], ref["acq"], excluded_rows(cand, x), q)
     if mode == "dense":
         return
     # the shard partition (distributed.shard_range over 4 ranks) reproduces the single call

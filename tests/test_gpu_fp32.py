@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle_np as O
+from fullref import cpu_full
 
 pytestmark = pytest.mark.gpu
 
@@ -69,15 +70,15 @@ def test_fp32_vs_f64_oracle(bo, n, dim, n_obj, m, ls):
                              topq=16, mode="fp32")
     torch.cuda.synchronize()
     got = {k: res[k].cpu().numpy() for k in ("mu", "var", "acq", "top_idx")}
-    sub = np.unique(np.r_[rng.choice(m, 1500, replace=False), got["top_idx"]])
-    ref = O.predict_acquire(x, y, cand[sub], pm, pv, lsv, betas, kinv=kinv)
+    # every candidate against the f64 CPU reference (oracle/cpu_ref.c)
+    ref = cpu_full(("fp32", n, dim, m), x, y, cand, kinv, pm, pv, lsv, betas)
     sq = np.sqrt(pv)[:, None]
-    dv = np.abs(got["var"][:, sub] - ref["var"]) / pv[:, None]
-    dm = np.abs(got["mu"][:, sub] - ref["mu"]) / sq
+    dv = np.abs(got["var"] - ref["var"]) / pv[:, None]
+    dm = np.abs(got["mu"] - ref["mu"]) / sq
     assert dv.max() <= VAR_TOL, dv.max()
     assert dm.max() <= VAR_TOL, dm.max()
     acq_tol = float(np.sum(1e-3 + betas * np.sqrt(VAR_TOL)))
-    da = np.abs(got["acq"][sub] - ref["acq"])
+    da = np.abs(got["acq"] - ref["acq"])
     assert da.max() <= acq_tol * max(1.0, np.abs(ref["acq"]).max()), da.max()
     assert np.median(da) <= 1e-4, np.median(da)
     # selection: 16 distinct, non-evaluated candidates whose reference acquisition is within the
@@ -86,6 +87,6 @@ def test_fp32_vs_f64_oracle(bo, n, dim, n_obj, m, ls):
     assert np.unique(top).size == 16 and (top >= 0).all()
     xs = {tuple(r) for r in x}
     assert not any(tuple(cand[i]) in xs for i in top)
-    ref_top = O.predict_acquire(x, y, cand[top], pm, pv, lsv, betas, kinv=kinv)["acq"]
-    full_ref_best = np.sort(ref["acq"][[tuple(cand[i]) not in xs for i in sub]])[::-1][:16]
+    ref_top = ref["acq"][top]
+    full_ref_best = np.sort(ref["acq"][[tuple(c) not in xs for c in cand]])[::-1][:16]
     assert ref_top.min() >= full_ref_best[-1] - 2 * acq_tol

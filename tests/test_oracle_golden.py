@@ -103,9 +103,9 @@ def test_cpu_ref_matches_oracle(golden, name):
     d = golden(name)
     kinv = kinv_of(d)
     out = cpu_ref.predict_acquire(d["x"], d["y"], d["cand"], kinv, d["pm"], d["pv"], d["ls"],
-                                  d["betas"], threads=4)
+                                  d["betas"], threads=4, ucb=True)
     from parity import check_predict
-    check_predict({k: out[k] for k in ("mu", "var", "acq")}, d, d["pv"])
+    check_predict({k: out[k] for k in ("mu", "var", "ucb", "acq")}, d, d["pv"])
     # the selection itself, with the reference's own acq values as input, is exact
     for q in (3, 16):
         sel = cpu_ref.select(d["acq"], d["cand"], d["x"], q)
