@@ -1,0 +1,956 @@
+// Internal header of the fused GP-posterior + acquisition + top-q kernels (bo_predict*.hip).
+//
+// Replaces the reference chain bayesopt/bayesian_optimization.py:145-207:
+//   update_k_star (numba_kernels.py:406-442) -> update_mean (:450-488) ->
+//   update_variance (:491-535) -> standardize_objectives (:538-570) ->
+//   update_ucb / update_hypervolume_improvement (acquisition.py:55-108) ->
+//   select_next_batch (acquisition.py:116-144, local top-q part).
+//
+// The chunk-major kernels are instantiated per padded input dimension in bo_predict_d{2,4,6,8}.hip
+// (parallel compilation); bo_predict.hip holds the preparation kernels, the merge kernels, the
+// planner and the C ABI.  DESIGN.md §3 describes the kernels.
+#pragma once
+
+#include "bo_common.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <type_traits>
+
+namespace bo {
+
+constexpr int kWaves = 4;               // waves per workgroup
+constexpr int kTile = 16 * kWaves;      // candidates per workgroup tile
+constexpr int kPanelSteps = 128;        // k-steps of 4 training rows per register panel (KMEM path)
+constexpr int kPF = 4;                  // W prefetch ring depth (pairs of k-steps)
+constexpr int kCMaxEp = 16;             // E-pairs (32 rows each) whose accumulators one wave holds
+constexpr int kC32MaxEp = 16;           // E-quads (64 rows each) per group of the f32 kernel
+constexpr int kExpTab = 256;            // 2^(j/256) table of exp2_tab
+// the dot-form exponent is used only while max|nl2| (max_f |x_f - z|^2 + max_c |c - z|^2) stays
+// below this bound: its cancellation error is ~4 eps times that, i.e. <= 1e-8 absolute in the
+// exponent (K* relative error 1e-8 against the 1e-5 pv variance tolerance)
+constexpr double kDotxLimit = 1.0e7;
+
+struct FusedArgs {
+  int n_obj, dim, n_train, n_pad;       // n_pad = padded training rows (multiple of 32 / 64)
+  int n_panels;                          // register panels of 512 rows (KMEM path only)
+  int n_excl;
+  int cand_kind, topq;
+  long long n_cand, cand_offset, ld_out, n_tiles;
+  long long grid_lo[BO_MAX_DIM], grid_shape[BO_MAX_DIM];
+  const void* cand;
+  const double* xpad;                    // [n_pad][DIM] training rows, padded rows = 1e200 (global)
+  const double* xc;                      // [n_pad][DIM] rows minus row 0 (the centre z) (global)
+  const double* sqg;                     // [n_pad] |xc_f|^2, inf for padded rows (global)
+  const unsigned long long* ext;         // [2] max |xc_f|^2 (f < N), max |c - z|^2 (bit patterns)
+  const double* excl;                    // [n_excl][DIM] evaluated points (global), NULL = x_train
+  const d2* wpack;                       // packed W (pack_cm_kernel / pack_kernel / pack32 layout)
+  unsigned int wpack_bytes;
+  const double* alpha;                   // [n_obj][n_pad] = K^-1 (y - pm) (global)
+  double pm[BO_MAX_OBJ], pv[BO_MAX_OBJ], nhl[BO_MAX_OBJ], beta[BO_MAX_OBJ], rsq_pv[BO_MAX_OBJ];
+  double *mu, *var, *std_mu, *std_var, *ucb, *acq;
+  TopEntry* partial;                     // [gridDim.x * kWaves][topq]
+  const double* kstar;                   // KMEM: materialised k_star [n_obj][ks_rows][n_cand]
+  long long ks_rows;
+  int upper;                             // W = upper triangle of sym(K^-1), diagonal halved
+  // separable K* on an integer grid: device flag (0 => usable), last-axis extent S and lower
+  // bound, LDS offsets (doubles) of the exp tables and per-wave row-factor scratch
+  const int* sep_flag;
+  int sep_S;
+  long long sep_lo;
+  int off_tbl, off_rw;
+  int rw_cache;                          // SEP row factors kept for every objective (LDS permitting)
+  int dotx;                              // explicit candidates, upper form: dot-form exponent allowed
+  int off_sq;                            // LDS offset (doubles) of |xc_f|^2 (LDS-resident rows)
+  int off_exp;                           // LDS offset (doubles) of the 2^(j/256) table
+};
+
+// Host-side plan of one bo_predict_acquire call (bo_predict.hip: make_plan).
+struct Plan {
+  int n_pad, ns, n_panels, dim_pad, n_excl;
+  bool multi;
+  size_t off_alpha, off_xpad, off_xc, off_sq, off_excl, off_partial, off_status, total;
+  bool cm;               // chunk-major kernel (cm_predict_kernel)
+  bool sep;              // ... with the integer-grid K* generation
+  bool grows;            // ... training rows / alpha read from global memory (N beyond LDS)
+  bool dotx;             // ... explicit candidates: dot-form exponent (subject to the device gate)
+  int off_tbl, off_rw;   // LDS offsets in doubles
+  bool rw_cache;         // SEP row factors cached per objective
+  bool fp32;             // cm32_predict_kernel (BO_PREDICT_FP32)
+  int off_sqlds, off_exp;
+  int grid, waves;       // persistent grid, waves per workgroup
+  long long n_tiles;
+  size_t lds;
+};
+
+// launch wrappers (one translation unit per padded dimension)
+hipError_t launch_cm_d2(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_cm_d4(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_cm_d6(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_cm_d8(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_c32_d2(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_c32_d4(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_c32_d6(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_c32_d8(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+
+}  // namespace bo
+
+namespace {
+
+using bo::FusedArgs;
+using bo::Plan;
+using bo::kWaves;
+using bo::kTile;
+using bo::kPF;
+using bo::kCMaxEp;
+using bo::kC32MaxEp;
+using bo::kExpTab;
+
+template <int DIM>
+__device__ __forceinline__ void load_candidate(const FusedArgs& a, long long j, bool valid,
+                                               double (&c)[DIM]) {
+#pragma unroll
+  for (int k = 0; k < DIM; ++k) c[k] = 0.0;
+  if (!valid) return;
+  if (a.cand_kind == BO_CAND_GRID) {
+    long long gi = a.cand_offset + j;
+#pragma unroll
+    for (int k = DIM - 1; k >= 0; --k) {
+      if (k < a.dim) {
+        const long long n = a.grid_shape[k];
+        const long long q = gi / n;
+        c[k] = (double)(a.grid_lo[k] + (gi - q * n));
+        gi = q;
+      }
+    }
+  } else if (a.cand_kind == BO_CAND_I64) {
+    const long long* p = (const long long*)a.cand + j * a.dim;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k)
+      if (k < a.dim) c[k] = (double)p[k];
+  } else {
+    const double* p = (const double*)a.cand + j * a.dim;
+#pragma unroll
+    for (int k = 0; k < DIM; ++k)
+      if (k < a.dim) c[k] = p[k];
+  }
+}
+
+// squared distance between row `row` of xs ([*][DIM], 16-B aligned) and the candidate;
+// numba_kernels.py:436-437 (diff = x_e - c_i, then diff . diff)
+template <int DIM>
+__device__ __forceinline__ double sqdist(const double* xs, int row, const double (&c)[DIM]) {
+  const d2* r = (const d2*)(xs + row * DIM);
+  double sq = 0.0;
+#pragma unroll
+  for (int k = 0; k < DIM / 2; ++k) {
+    const d2 x = r[k];
+    const double d0 = x.x - c[2 * k], d1 = x.y - c[2 * k + 1];
+    sq = __builtin_fma(d0, d0, sq);
+    sq = __builtin_fma(d1, d1, sq);
+  }
+  return sq;
+}
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Fence between the last MFMA of a contraction and the first read of its accumulators.
+// hipcc's gfx950 hazard recognizer under-counts the wait states a VALU / v_accvgpr_read needs
+// after v_mfma_f64_16x16x4_f64 when the reading block is reached through a branch that skips
+// another block (observed: stale rows of the last MFMA, deterministic data-dependent errors
+// up to 0.15 pv).  The asm consumes and "redefines" both accumulators in place, so it cannot be
+// scheduled before the MFMAs that produce them and no read of them can be hoisted above it;
+// its 64 wait states cover the MFMA's full latency.
+template <bool AGPR, int NOPS = 64>
+__device__ __forceinline__ void mfma_fence(d4& x, d4& y) {
+#define BO_NOPS8 "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+  if (NOPS == 0) {
+    if (AGPR) asm volatile("" : "+a"(x), "+a"(y));
+    else asm volatile("" : "+v"(x), "+v"(y));
+  } else {
+    if (AGPR) asm volatile(BO_NOPS8 : "+a"(x), "+a"(y));
+    else asm volatile(BO_NOPS8 : "+v"(x), "+v"(y));
+  }
+#undef BO_NOPS8
+}
+
+// vmcnt(n) with expcnt / lgkmcnt left at their maxima (gfx9 s_waitcnt encoding)
+#define BO_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | 0x70 | 0xF00)
+
+__device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+__device__ __forceinline__ void prime_ring(__amdgpu_buffer_rsrc_t wr, int voff, int base,
+                                           d2 (&wa)[kPF], d2 (&wb)[kPF]) {
+#pragma unroll
+  for (int p = 0; p < kPF; ++p) {
+    wa[p] = wload(wr, voff, base + (p << 11));
+    wb[p] = wload(wr, voff, base + (p << 11) + 1024);
+  }
+}
+
+// 2^t for the K* exponents (t <= a few tens; -inf / very negative -> exactly 0), with the
+// 2^(j/256) table `tb` in LDS: t = n + j/256 + r, |r| <= 1/512; 2^r by its degree-4 Taylor
+// polynomial in r ln 2 (|term 5| < 4e-17 relative).  The round-to-nearest k = 256 t comes from
+// the 1.5 * 2^52 shifter, whose low 32 bits hold k in two's complement (j = k & 255, n = k >> 8).
+// 10 f64 operations (the libm-style exp costs ~20).
+__device__ __forceinline__ double exp2_tab(double t, const double* tb) {
+  const double x = fmax(t, -1075.0);
+  const double s = __builtin_fma(x, 256.0, 6755399441055744.0);
+  const int ki = (int)__double_as_longlong(s);
+  const double kd = s - 6755399441055744.0;
+  const double r = __builtin_fma(kd, -0.00390625, x);
+  double p = __builtin_fma(9.6181291076284772e-03, r, 5.5504108664821580e-02);
+  p = __builtin_fma(p, r, 2.4022650695910071e-01);
+  p = __builtin_fma(p, r, 6.9314718055994531e-01);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_ldexp(p * tb[ki & (kExpTab - 1)], ki >> 8);
+}
+
+// Nested guards over the unrolled E-pair bodies: body E runs iff E < n, and is entered only
+// from body E - 1 (see chunk_step in cm_tiles).
+template <int E, int N>
+struct EpChain {
+  template <class F>
+  static __device__ __forceinline__ void run(F& f, int n) {
+    if (E < n) {
+      f(std::integral_constant<int, E>{});
+      EpChain<E + 1, N>::run(f, n);
+    }
+  }
+};
+template <int N>
+struct EpChain<N, N> {
+  template <class F>
+  static __device__ __forceinline__ void run(F&, int) {}
+};
+
+// K* values K*[f][j] = pv exp(-0.5 |x_f - c_j|^2 / ls^2) (numba_kernels.py:436-442) of lane j.
+//   SEP (integer 'ij' grid): rv[f] * T[rb[f] - jl] (row factor times the last-axis table);
+//   otherwise the exponent in base 2 with pv folded in, t = nl2 |x_f - c|^2 + log2 pv
+//   (nl2 = nhl log2 e), then exp2_tab.  Coordinates are CENTRED on z = training row 0 (xs holds
+//   x_f - z, c is c - z): distances are translation invariant and the centring keeps the dot
+//   form below exact enough for coordinates far from the origin.
+//   DOTX: t = nl2 |x_f|^2 + (nl2 |c|^2 + log2 pv) + sum_k x_fk (-2 nl2 c_k), |x_f|^2 from sq[]:
+//   DIM + 1 FMAs instead of 2 DIM + 1; used only under the kDotxLimit gate.
+template <int DIM, bool SEP, bool DOTX = false>
+struct KRows {
+  const double* sq;   // DOTX: [n_pad] |x_f|^2 (inf for padded rows)
+  double cj, nl2, lpv, dk[DIM];
+  const double* rv;   // SEP: [n_pad] pv * R(f) (0 for padded rows)
+  const int* rb;      // SEP: [n_pad] table index base (x_f,last - lo_last) + S - 1; jl = col0 + lane
+  const double* tb;   // SEP: objective's table T; otherwise the 2^(j/256) table
+  const double* xs;   // !SEP: training rows [n_pad][DIM] (padded rows at 1e200)
+  double c[DIM];      // !SEP: this lane's candidate
+  int jl;
+  __device__ __forceinline__ double at(int f) const {
+    if (SEP) return rv[f] * tb[rb[f] - jl];
+    if (DOTX) {
+      const d2* r = (const d2*)(xs + f * DIM);
+      double t = __builtin_fma(nl2, sq[f], cj);
+#pragma unroll
+      for (int k = 0; k < DIM / 2; ++k) {
+        const d2 x = r[k];
+        t = __builtin_fma(x.x, dk[2 * k], t);
+        t = __builtin_fma(x.y, dk[2 * k + 1], t);
+      }
+      return exp2_tab(t, tb);
+    }
+    return exp2_tab(__builtin_fma(sqdist<DIM>(xs, f, c), nl2, lpv), tb);
+  }
+  // the 8 values of 32-row chunk `ch` this lane feeds to the MFMAs: rows 32 ch + 4 s + g
+  __device__ __forceinline__ void chunk(int ch, int g, double (&B)[8]) const {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) B[s] = at(32 * ch + 4 * s + g);
+  }
+};
+
+// Next-chunk generation split into three stages that chunk_step places between the MFMA
+// pairs of the chunk's first E-pair (sched barriers pin them), so that every LDS round trip
+// of the generation (SEP: row factor + table index, then the table value; the alpha values
+// of the mean) completes under MFMAs instead of stalling the wave before the chunk:
+//   s0: rv[f], rb[f], alpha[f] loads     s1: table loads T[rb - jl]     s2: the products.
+// The exp path (!SEP) is VALU work that serialises with f64 MFMAs anyway: all of it in s2.
+template <int DIM, bool SEP, bool DOTX = false>
+struct KGen {
+  using KR = KRows<DIM, SEP, DOTX>;
+  double rv[8], tv[8];
+  int rb[8];
+  __device__ __forceinline__ void s0(const KR& K, const double* al, bool mu_on, int ch,
+                                     int g, double (&A)[8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int f = 32 * ch + 4 * s + g;
+      const double a = al[f];
+      A[s] = mu_on ? a : 0.0;
+      if (SEP) { rv[s] = K.rv[f]; rb[s] = K.rb[f]; }
+    }
+  }
+  // s0 without the alpha values (the variance epilogue's regeneration)
+  __device__ __forceinline__ void s0k(const KR& K, int ch, int g) {
+    if (SEP) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int f = 32 * ch + 4 * s + g;
+        rv[s] = K.rv[f];
+        rb[s] = K.rb[f];
+      }
+    }
+  }
+  __device__ __forceinline__ void s1(const KR& K) {
+    if (SEP) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) tv[s] = K.tb[rb[s] - K.jl];
+    }
+  }
+  __device__ __forceinline__ void s2(const KR& K, int ch, int g, double (&B)[8]) {
+    if (SEP) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) B[s] = rv[s] * tv[s];
+    } else {
+      K.chunk(ch, g, B);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// Chunk-major fused kernel: the production path.
+//
+// f64 MFMAs and f64 VALU instructions share the SIMD's DP pipe (measured on MI355X: they
+// serialise even across waves), so the time of this kernel is  sum(MFMA) + sum(f64 VALU).
+// The loop order is therefore chosen to generate every K* value exactly ONCE per group:
+//   for each 32-row chunk c of K* (rows 32c .. 32c+31, 8 values per lane):
+//       generate K*[chunk c][16 candidates]  (B operand, registers)
+//       for each E-pair ep (32 rows of W) that touches chunk c  -- all 16, or ep <= c when
+//       W is upper triangular:   acc[ep] += W[ep-rows, chunk c] . K*[chunk c]
+// with the accumulators of all (up to 16) E-pairs resident (256 AGPRs, one wave per SIMD).
+// The W stream is packed in exactly this (c, ep, k-step pair) order and streamed from L2
+// through a 4-deep register ring; the next chunk's K* is generated while the current chunk's
+// MFMAs run.  Per 16-MFMA E-pair block there is no VALU work at all.
+//
+// Variance forms (the reference: q = k . (K^-1 k), update_variance numba_kernels.py:521-529):
+//   upper (default): q = 2 k . (U k) with U = upper triangle of sym(K^-1) = (K^-1 + K^-T)/2,
+//     diagonal halved -- exactly k^T K^-1 k in exact arithmetic (k^T A k = k^T sym(A) k), half
+//     the MFMAs, no factorisation;
+//   dense: z = K^-1 k verbatim; q = k . z after the last chunk (chunk ep regenerated).
+//
+// GROWS: the training rows, |x_f|^2 and alpha are read from global memory (L2-resident)
+// instead of LDS, for N whose rows do not fit the 160 KiB LDS (the reference has no N cap).
+// ---------------------------------------------------------------------------------------
+template <int DIM, bool SEP, bool UPPER, bool DOTX, bool GROWS>
+__device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
+  constexpr bool upper = UPPER;
+  // training rows (SEP: original grid coordinates; otherwise centred on z = row 0), alpha
+  const double* xs = GROWS ? a.xc : smem;
+  const double* alpha = GROWS ? a.alpha : smem + (size_t)a.n_pad * DIM;
+  const double* sqv = GROWS ? a.sqg : smem + a.off_sq;
+  const double* etab = smem + a.off_exp;                    // 2^(j/256) (!SEP)
+  const double* tbl = smem + a.off_tbl;                     // [n_obj][2S - 1] (SEP)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, jl = lane & 15;
+  // SEP row factors, per wave: rv[nslot][n_pad] = pv_o R(f) (one slot per objective when they
+  // are cached across the tiles of a grid row, else one slot rebuilt per objective and tile),
+  // then rb[n_pad] = table index base (x_f,last - lo_last) + S - 1 and on[n_pad] = "training
+  // point f lies on this grid row" (all other coordinates equal)
+  const int nslot = a.rw_cache ? a.n_obj : 1;
+  double* rv = smem + a.off_rw + (size_t)wave * a.n_pad * (nslot + 1);
+  int* rb = (int*)(rv + (size_t)nslot * a.n_pad);
+  int* on = rb + a.n_pad;
+  long long cur_row = -1;
+  const int TS = 2 * a.sep_S - 1;
+  const int nch = a.n_pad / 32;
+  const int last = a.dim - 1;
+  const int w_obj = a.n_pad * a.n_pad * 8;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
+  const int voff = lane * 16;
+  // the centre z (training row 0) of the non-SEP generation
+  double z[DIM];
+#pragma unroll
+  for (int k = 0; k < DIM; ++k) z[k] = SEP ? 0.0 : a.xpad[k];
+
+  double top_v = -__builtin_inf();
+  long long top_i = -1;
+  // SEP: contiguous tile ranges per workgroup, so that a wave walks along grid rows and its
+  // row factors are rebuilt once per row (every S / 64 tiles) instead of once per tile;
+  // otherwise grid-strided tiles
+  const long long tpw = (a.n_tiles + gridDim.x - 1) / gridDim.x;
+  const long long t_first = SEP ? blockIdx.x * tpw : blockIdx.x;
+  const long long t_end = SEP ? (t_first + tpw < a.n_tiles ? t_first + tpw : a.n_tiles) : a.n_tiles;
+  const long long t_step = SEP ? 1 : gridDim.x;
+  // row pass (numba_kernels.py:436-442 split along the grid): per training row f, the squared
+  // distance over the non-last coordinates is shared by the wave's 16 candidates
+  auto row_pass = [&](const double (&c)[DIM], int o_lo, int o_hi) {
+    __builtin_amdgcn_wave_barrier();
+    for (int f = lane; f < a.n_pad; f += 64) {
+      int b = a.sep_S - 1, onrow = 0;                      // padded rows: any in-range index, v = 0
+      double sqs = 0.0;
+      if (f < a.n_train) {
+        const double* r = xs + f * DIM;
+        double xl = 0.0;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) {
+          if (k == last) xl = r[k];
+          else { const double d = r[k] - c[k]; sqs = __builtin_fma(d, d, sqs); }
+        }
+        b = (int)(xl - (double)a.sep_lo) + a.sep_S - 1;
+        onrow = sqs == 0.0;
+      }
+      for (int o = o_lo; o < o_hi; ++o)
+        rv[(size_t)(o - o_lo) * a.n_pad + f] = f < a.n_train ? a.pv[o] * exp(sqs * a.nhl[o]) : 0.0;
+      rb[f] = b;
+      on[f] = onrow;
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (long long tile = t_first; tile < t_end; tile += t_step) {
+    const long long j = tile * kTile + wave * 16 + jl;
+    const bool valid = j < a.n_cand;
+    double c[DIM];
+    int col0 = 0;                 // SEP: the wave's first candidate's offset on the last axis
+    if (SEP) {
+      // the wave's 16 candidates: one grid row, consecutive along the last axis
+      const long long j0 = tile * kTile + wave * 16;
+      const long long jj = j0 < a.n_cand ? j0 : 0;
+      load_candidate<DIM>(a, jj, true, c);
+#pragma unroll
+      for (int k = 0; k < DIM; ++k)
+        if (k == last) { col0 = (int)(c[k] - (double)a.sep_lo); c[k] += (double)jl; }
+      if (a.rw_cache) {
+        const long long row = (a.cand_offset + jj) / a.sep_S;
+        if (row != cur_row) { row_pass(c, 0, a.n_obj); cur_row = row; }
+      }
+    } else {
+      load_candidate<DIM>(a, j, valid, c);
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) c[k] -= z[k];
+    }
+    double acq = 0.0;
+    for (int o = 0; o < a.n_obj; ++o) {
+      if (SEP && !a.rw_cache) row_pass(c, o, o + 1);
+      KRows<DIM, SEP, DOTX> K;
+      K.rv = rv + (a.rw_cache ? (size_t)o * a.n_pad : 0); K.rb = rb;
+      K.tb = SEP ? tbl + (size_t)o * TS : etab;
+      K.xs = xs;
+      K.nl2 = a.nhl[o] * 1.4426950408889634;
+      K.lpv = log2(a.pv[o]);
+      K.jl = SEP ? col0 + jl : jl;   // T index = rb[f] - (col0 + jl) = x_f,last - c_last + S - 1
+#pragma unroll
+      for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
+      if (DOTX) {
+        K.sq = sqv;
+        double cc = 0.0;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) { cc = __builtin_fma(c[k], c[k], cc); K.dk[k] = -2.0 * K.nl2 * c[k]; }
+        K.cj = __builtin_fma(K.nl2, cc, K.lpv);
+      }
+      const double* al = alpha + (size_t)o * a.n_pad;
+      const int base = o * w_obj;
+      d2 wa[kPF], wb[kPF];
+      prime_ring(wr, voff, base, wa, wb);
+      int pos = 0;
+      double mpart = 0.0, qpart = 0.0;
+      d4 acc[kCMaxEp][2];
+      // E-pairs in groups of kCMaxEp (the accumulators one wave holds: 512 rows); a group
+      // streams the chunks that touch it (c >= its first E-pair when upper, all otherwise) and
+      // regenerates their K*.  One group when N <= 512.
+      for (int e0 = 0; e0 < nch; e0 += kCMaxEp) {
+        const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
+#pragma unroll
+        for (int e = 0; e < kCMaxEp; ++e) {
+          acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
+          acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
+        }
+        // one chunk: MFMAs from register set B while the next chunk's K* (and its alpha
+        // values, An) is generated into Bn in three stages inside E-pair 0's MFMA stream (the
+        // sets alternate: no register copies between the chunks).  Branch-free: the last chunk
+        // regenerates itself (chn clamped) and groups after the first add 0 x alpha to mu.
+        const bool mu_on = e0 == 0;
+        KGen<DIM, SEP, DOTX> gen;
+        auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8], const double (&A)[8],
+                              double (&An)[8]) {
+          // next chunk: ascending (dense) / descending (upper); the last one regenerates itself
+          const int chn = upper ? (ch > e0 ? ch - 1 : ch) : (ch + 1 < nch ? ch + 1 : ch);
+          // the group's E-pairs touching chunk ch, ascending: the first n_here of them (e0 + e
+          // <= ch when upper).  EpChain nests the guards (body e+1 is reached only from body e),
+          // so every body has one predecessor and hipcc's vmcnt waits inside the chunk stay
+          // exact; independent guards made every body a join and cost a vmcnt(0) drain of the
+          // W ring per E-pair.
+          const int n_here = upper ? (ch - e0 + 1 < eN ? ch - e0 + 1 : eN) : eN;
+          auto ep_body = [&](auto e_c) {
+            constexpr int e = decltype(e_c)::value;
+            if constexpr (e == 0) {
+              gen.s0(K, al, mu_on, chn, g, An);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int pp = 0; pp < 4; ++pp) {
+              // MFMAs first, then the refill of the same ring slot (no operand copies)
+              acc[e][0] = mfma64(wa[pp].x, B[2 * pp], acc[e][0]);
+              acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
+              acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
+              acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
+              const int so = base + ((pos + kPF) << 11);
+              wa[pp] = wload(wr, voff, so);
+              wb[pp] = wload(wr, voff, so + 1024);
+              ++pos;
+              if constexpr (e == 0) {
+                if (pp == 0) {
+                  __builtin_amdgcn_sched_barrier(0);
+                  gen.s1(K);
+                  __builtin_amdgcn_sched_barrier(0);
+                } else if (pp == 1) {
+                  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                  for (int s = 0; s < 8; ++s) mpart = __builtin_fma(A[s], B[s], mpart);
+                  __builtin_amdgcn_sched_barrier(0);
+                } else if (pp == 2) {
+                  __builtin_amdgcn_sched_barrier(0);
+                  gen.s2(K, chn, g, Bn);
+                  __builtin_amdgcn_sched_barrier(0);
+                }
+              }
+            }
+            // upper: E-pair e0 + e is complete after its own chunk (chunks descend), the last
+            // body of that chunk: q += K*[chunk rows] . acc with the rows still in B (rows
+            // 32 ep + g + 4r (+16) = B slots r (4 + r)); no regeneration
+            if constexpr (UPPER) {
+              if (ch - e0 == e) {
+                mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  qpart = __builtin_fma(B[r], acc[e][0][r], qpart);
+                  qpart = __builtin_fma(B[4 + r], acc[e][1][r], qpart);
+                }
+              }
+            }
+          };
+          EpChain<0, kCMaxEp>::run(ep_body, n_here);
+        };
+        const int c0 = upper ? nch - 1 : 0;
+        double BX[8], BY[8], AX[8], AY[8];
+        K.chunk(c0, g, BX);
+#pragma unroll
+        for (int s = 0; s < 8; ++s) AX[s] = mu_on ? al[32 * c0 + 4 * s + g] : 0.0;
+        int ch = c0;
+        if (upper) {
+          for (; ch - 1 >= e0; ch -= 2) {
+            chunk_step(ch, BX, BY, AX, AY);
+            chunk_step(ch - 1, BY, BX, AY, AX);
+          }
+          if (ch >= e0) chunk_step(ch, BX, BY, AX, AY);
+        } else {
+          for (; ch + 1 < nch; ch += 2) {
+            chunk_step(ch, BX, BY, AX, AY);
+            chunk_step(ch + 1, BY, BX, AY, AX);
+          }
+          if (ch < nch) chunk_step(ch, BX, BY, AX, AY);
+        }
+        // dense: q = k . z after the last chunk, chunk ep's K* regenerated.  Software-pipelined:
+        // E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence and multiplied after
+        // its FMAs, so the fences' wait states cover the LDS round trips.
+        if (!upper) {
+          KGen<DIM, SEP, DOTX> gq[2];
+          double S[2][8];
+          gq[0].s0k(K, e0, g);
+          gq[0].s1(K);
+          gq[0].s2(K, e0, g, S[0]);
+#pragma unroll
+          for (int e = 0; e < kCMaxEp; ++e) {
+            if (e < eN) {
+              const int cur = e & 1, nxt = cur ^ 1;
+              const bool more = e + 1 < eN;
+              if (more) gq[nxt].s0k(K, e0 + e + 1, g);
+              mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+              if (more) gq[nxt].s1(K);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                qpart = __builtin_fma(S[cur][r], acc[e][0][r], qpart);
+                qpart = __builtin_fma(S[cur][4 + r], acc[e][1][r], qpart);
+              }
+              if (more) gq[nxt].s2(K, e0 + e + 1, g, S[nxt]);
+            }
+          }
+        }
+      }
+      if (upper) qpart *= 2.0;
+      qpart += __shfl_xor(qpart, 16, 64);
+      qpart += __shfl_xor(qpart, 32, 64);
+      mpart += __shfl_xor(mpart, 16, 64);
+      mpart += __shfl_xor(mpart, 32, 64);
+      const double pv = a.pv[o], pm = a.pm[o];
+      const double mu = pm + mpart;                                   // :486-488
+      const double var = fmax(pv - qpart, BO_MIN_VARIANCE);           // :532-535
+      const double smu = (mu - pm) / a.rsq_pv[o];                      // :563-565
+      const double svar = var / pv;                                    // :568-570
+      const double u = smu + a.beta[o] * sqrt(fabs(svar));             // acquisition.py:52
+      acq = (o == 0) ? u : acq + u;                                    // acquisition.py:108
+      if (valid && g == 0) {
+        const long long off = (long long)o * a.ld_out + j;
+        if (a.mu) a.mu[off] = mu;
+        if (a.var) a.var[off] = var;
+        if (a.std_mu) a.std_mu[off] = smu;
+        if (a.std_var) a.std_var[off] = svar;
+        if (a.ucb) a.ucb[off] = u;
+      }
+    }
+    if (valid && g == 0 && a.acq) a.acq[j] = acq;
+    if (a.topq > 0) {
+      // exclusion of evaluated points (acquisition.py:137-139: all coordinates equal)
+      bool hit = false;
+      if (SEP && !a.excl) {
+        // training points on this grid row whose last coordinate falls in the wave's 16
+        // columns; OR over the wave, bit jl is this lane's candidate
+        unsigned int xmask = 0;
+        for (int f = lane; f < a.n_train; f += 64) {
+          const int dx = rb[f] - (a.sep_S - 1) - col0;
+          if (on[f] && dx >= 0 && dx < 16) xmask |= 1u << dx;
+        }
+        unsigned int m = xmask;
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) m |= (unsigned int)__shfl_xor((int)m, sh, 64);
+        hit = (m >> jl) & 1u;
+      } else {
+        // only candidates that would enter the wave's top-q are compared, exactly, in their
+        // original coordinates against the evaluated points in global memory; lane group g
+        // checks points g, g + 4, ...
+        const long long gi0 = valid ? a.cand_offset + j : -1;
+        const double tv = __shfl(top_v, a.topq - 1, 64);
+        const long long ti = __shfl(top_i, a.topq - 1, 64);
+        const bool need = gi0 >= 0 && bo_better(acq, gi0, tv, ti);
+        if (__ballot(need) != 0ull) {
+          double co[DIM];
+          load_candidate<DIM>(a, j, valid, co);
+          const double* es = a.excl ? a.excl : a.xpad;
+          const int ne = a.excl ? a.n_excl : a.n_train;
+          for (int e = g; e < ne; e += 4) {
+            const double* r = es + (size_t)e * DIM;
+            bool eq = true;
+#pragma unroll
+            for (int k = 0; k < DIM; ++k) eq = eq && (r[k] == co[k]);
+            hit = hit || eq;
+          }
+        }
+      }
+      const unsigned long long hb = __ballot(hit);
+      const bool excluded =
+          ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
+      const long long gi = (valid && !excluded) ? a.cand_offset + j : -1;
+      bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+    }
+  }
+  BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
+  if (a.topq > 0 && lane < a.topq) {
+    TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
+    dst[lane].v = top_v;
+    dst[lane].i = top_i;
+  }
+}
+
+// GRID: the host found the grid structure usable (rows of 16); the device flag then says
+// whether every training point lies on the grid's last axis (sep_check in the prep kernel).
+// GROWS: training rows / alpha stay in global memory (N beyond the LDS budget).
+template <int DIM, bool GRID, bool UPPER, bool GROWS>
+__global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x;
+  const bool sep = !GROWS && GRID && __builtin_amdgcn_readfirstlane(*a.sep_flag) == 0;
+  if (!GROWS) {
+    // rows: original grid coordinates for the row pass (SEP), centred otherwise
+    const double* src = sep ? a.xpad : a.xc;
+    for (int t = tid; t < a.n_pad * DIM; t += blockDim.x) smem[t] = src[t];
+    double* alpha = smem + (size_t)a.n_pad * DIM;
+    for (int t = tid; t < a.n_obj * a.n_pad; t += blockDim.x) alpha[t] = a.alpha[t];
+  }
+  if (sep) {
+    double* tbl = smem + a.off_tbl;
+    const int TS = 2 * a.sep_S - 1;
+    for (int t = tid; t < a.n_obj * TS; t += blockDim.x) {
+      const int o = t / TS;
+      const double m = (double)(t - o * TS - (a.sep_S - 1));
+      tbl[t] = exp(a.nhl[o] * (m * m));
+    }
+  } else {
+    for (int t = tid; t < kExpTab; t += blockDim.x) smem[a.off_exp + t] = exp2((double)t / kExpTab);
+    if (!GROWS && a.dotx)
+      for (int f = tid; f < a.n_pad; f += blockDim.x) smem[a.off_sq + f] = a.sqg[f];
+  }
+  // dot-form gate (explicit candidates): max|nl2| (max_f |x_f - z|^2 + max_c |c - z|^2) over
+  // the training rows and the call's candidates (prep kernels, bit patterns of non-negative
+  // doubles max-reduced as integers; NaN compares false) must stay below kDotxLimit
+  bool dotx = false;
+  if (!GRID && UPPER && a.dotx) {
+    const double rx = __longlong_as_double((long long)a.ext[0]);
+    const double rc = __longlong_as_double((long long)a.ext[1]);
+    double nl = 0.0;
+    for (int o = 0; o < a.n_obj; ++o) nl = fmax(nl, fabs(a.nhl[o] * 1.4426950408889634));
+    dotx = nl * (rx + rc) <= bo::kDotxLimit;
+  }
+  __syncthreads();
+  if constexpr (GRID && !GROWS) {
+    if (sep) { cm_tiles<DIM, true, UPPER, false, false>(a, smem); return; }
+  }
+  if constexpr (!GRID && UPPER) {
+    if (dotx) { cm_tiles<DIM, false, UPPER, true, GROWS>(a, smem); return; }
+  }
+  cm_tiles<DIM, false, UPPER, false, GROWS>(a, smem);
+}
+
+template <int DIM, bool GRID, bool UPPER, bool GROWS>
+hipError_t launch_cm_k(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) {
+  auto k = cm_predict_kernel<DIM, GRID, UPPER, GROWS>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, fa);
+  return hipGetLastError();
+}
+
+template <int DIM, bool UPPER, bool GROWS>
+hipError_t launch_cm_u(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  if constexpr (GROWS) return launch_cm_k<DIM, false, UPPER, true>(fa, pl.grid, pl.lds, st);
+  return pl.sep ? launch_cm_k<DIM, true, UPPER, false>(fa, pl.grid, pl.lds, st)
+                : launch_cm_k<DIM, false, UPPER, false>(fa, pl.grid, pl.lds, st);
+}
+
+template <int DIM>
+hipError_t launch_cm(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  if (fa.upper)
+    return pl.grows ? launch_cm_u<DIM, true, true>(pl, fa, st) : launch_cm_u<DIM, true, false>(pl, fa, st);
+  return pl.grows ? launch_cm_u<DIM, false, true>(pl, fa, st) : launch_cm_u<DIM, false, false>(pl, fa, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// fp32 variant (BO_PREDICT_FP32; BASELINE config C5 "fp32 with fp64 reference check"):
+// the upper form q = 2 k.(U k) on v_mfma_f32_16x16x4_f32 (32 cycles per MFMA per SIMD, twice
+// the f64 rate), K* = 2^(nhl log2e |x_f - c_j|^2 + log2 pv) on v_exp_f32 over coordinates
+// centred on training row 0 (f32 keeps only ~7 digits of absolute coordinates), mu / q
+// accumulated in f32 and everything after them (variance floor, standardisation, UCB, sum,
+// top-q) in f64.
+//
+// Body = E-quad: 64 rows of U (4 MFMA row blocks b), chunk = 64 rows of K* (16 k-steps).
+// f32 D layout (lane l holds D[4 (l >> 4) + r][l & 15]) differs from f64's, so the K* row fed
+// at k-step s by lane group g is permuted: f(s, g) = 64 c + 16 (s >> 2) + 4 g + (s & 3).  Then
+// the rows a completing E-quad's accumulator block b holds in its lane (64 ep + 16 b + 4 g + r)
+// are exactly B slots s = 4 b + r of chunk ep: the in-register epilogue of the f64 kernel.
+// Chunks descend (E-quad ep is complete at chunk ep); W streams per (group, chunk, E-quad,
+// k-quad kq, block b) as one 16-B float4 per lane (k-steps 4 kq .. 4 kq + 3), through a
+// 16-entry register ring that holds exactly one E-quad block (static slot indices).
+// Exclusion of evaluated points is tested (exactly, in f64 from HBM) only for candidates that
+// would enter the wave's top-q.
+// ---------------------------------------------------------------------------------------
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mfma32(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 wload32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void mfma_fence32(f4& a, f4& b, f4& c, f4& d) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+               : "+a"(a), "+a"(b), "+a"(c), "+a"(d));
+}
+
+// (chunk, E-quad) blocks of group e0, upper form
+__host__ __device__ inline long long c32_group_blocks(int nch, int e0) {
+  const int eN = nch - e0 < kC32MaxEp ? nch - e0 : kC32MaxEp;
+  return (long long)(eN - 1) * eN / 2 + (long long)(nch - e0 - eN + 1) * eN;
+}
+__host__ __device__ inline long long c32_blocks(int nch) {
+  long long b = 0;
+  for (int e0 = 0; e0 < nch; e0 += kC32MaxEp) b += c32_group_blocks(nch, e0);
+  return b;
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem32[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, jl = lane & 15;
+  float* xs = smem32;                                        // [n_pad][DIM] centred rows
+  float* al = xs + (size_t)a.n_pad * DIM;                    // [n_obj][n_pad]
+  for (int t = tid; t < a.n_pad * DIM; t += blockDim.x) xs[t] = (float)a.xc[t];   // 1e200 -> inf
+  for (int t = tid; t < a.n_obj * a.n_pad; t += blockDim.x) al[t] = (float)a.alpha[t];
+  __syncthreads();
+  double z[DIM];
+#pragma unroll
+  for (int k = 0; k < DIM; ++k) z[k] = a.xpad[k];
+  const int nch = a.n_pad / 64;
+  const long long w_obj = c32_blocks(nch) * 1024 * 16;       // bytes per objective
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
+  const int voff = lane * 16;
+  const double* es = a.excl ? a.excl : a.xpad;               // f64 [*][DIM] (exact equality)
+  const int ne = a.excl ? a.n_excl : a.n_train;
+  double top_v = -__builtin_inf();
+  long long top_i = -1;
+  for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    const long long j = tile * kTile + wave * 16 + jl;
+    const bool valid = j < a.n_cand;
+    double c[DIM];
+    load_candidate<DIM>(a, j, valid, c);
+    float c32[DIM];
+#pragma unroll
+    for (int k = 0; k < DIM; ++k) c32[k] = (float)(c[k] - z[k]);
+    double acq = 0.0;
+    for (int o = 0; o < a.n_obj; ++o) {
+      const float nl2 = (float)(a.nhl[o] * 1.4426950408889634);
+      const float lpv = (float)log2(a.pv[o]);
+      auto kval = [&](int f) -> float {
+        const float* r = xs + f * DIM;
+        float d2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DIM; ++k) { const float d = r[k] - c32[k]; d2 = __builtin_fmaf(d, d, d2); }
+        return __builtin_amdgcn_exp2f(__builtin_fmaf(d2, nl2, lpv));
+      };
+      auto chunk = [&](int ch, float (&B)[16]) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) B[s] = kval(64 * ch + 16 * (s >> 2) + 4 * g + (s & 3));
+      };
+      const float* alo = al + (size_t)o * a.n_pad;
+      const int base = (int)(o * w_obj);
+      f4 w[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) w[q] = wload32(wr, voff, base + q * 1024);
+      int pos = 0;
+      float mpart = 0.0f, qpart = 0.0f;
+      f4 acc[kC32MaxEp][4];
+      for (int e0 = 0; e0 < nch; e0 += kC32MaxEp) {
+        const int eN = nch - e0 < kC32MaxEp ? nch - e0 : kC32MaxEp;
+#pragma unroll
+        for (int e = 0; e < kC32MaxEp; ++e)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[e][b] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+        const bool mu_on = e0 == 0;
+        auto chunk_step = [&](int ch, const float (&B)[16], float (&Bn)[16]) {
+          const int chn = ch > e0 ? ch - 1 : ch;
+          const int n_here = ch - e0 + 1 < eN ? ch - e0 + 1 : eN;
+          auto ep_body = [&](auto e_c) {
+            constexpr int e = decltype(e_c)::value;
+            // keep the workgroup's 4 waves on the same E-quad block: they stream identical W
+            // data, so the lockstep turns 3 of 4 L2 reads into L1 hits (C5: W = 8.6 MB per
+            // objective does not fit an XCD's L2; measured 141 -> 108 ms per 2^20 candidates)
+            __builtin_amdgcn_s_barrier();
+            if constexpr (e == 0) {
+              // branch-free (a join here would drain the W ring with vmcnt(0))
+#pragma unroll
+              for (int s = 0; s < 16; ++s) {
+                const float av = alo[64 * ch + 16 * (s >> 2) + 4 * g + (s & 3)];
+                mpart = __builtin_fmaf(mu_on ? av : 0.0f, B[s], mpart);
+              }
+              chunk(chn, Bn);
+            }
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) acc[e][b] = mfma32(w[4 * kq + b][t], B[4 * kq + t], acc[e][b]);
+              const int so = base + (pos + 1) * 16384 + kq * 4096;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) w[4 * kq + b] = wload32(wr, voff, so + b * 1024);
+            }
+            ++pos;
+            if (ch - e0 == e) {
+              mfma_fence32(acc[e][0], acc[e][1], acc[e][2], acc[e][3]);
+#pragma unroll
+              for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) qpart = __builtin_fmaf(B[4 * b + r], acc[e][b][r], qpart);
+            }
+          };
+          EpChain<0, kC32MaxEp>::run(ep_body, n_here);
+        };
+        float BX[16], BY[16];
+        chunk(nch - 1, BX);
+        int ch = nch - 1;
+        for (; ch - 1 >= e0; ch -= 2) {
+          chunk_step(ch, BX, BY);
+          chunk_step(ch - 1, BY, BX);
+        }
+        if (ch >= e0) chunk_step(ch, BX, BY);
+      }
+      qpart += __shfl_xor(qpart, 16, 64);
+      qpart += __shfl_xor(qpart, 32, 64);
+      mpart += __shfl_xor(mpart, 16, 64);
+      mpart += __shfl_xor(mpart, 32, 64);
+      const double pv = a.pv[o], pm = a.pm[o];
+      const double mu = pm + (double)mpart;                               // :486-488
+      const double var = fmax(pv - 2.0 * (double)qpart, BO_MIN_VARIANCE);  // :532-535
+      const double smu = (mu - pm) / a.rsq_pv[o];                         // :563-565
+      const double svar = var / pv;                                       // :568-570
+      const double u = smu + a.beta[o] * sqrt(fabs(svar));                // acquisition.py:52
+      acq = (o == 0) ? u : acq + u;                                       // acquisition.py:108
+      if (valid && g == 0) {
+        const long long off = (long long)o * a.ld_out + j;
+        if (a.mu) a.mu[off] = mu;
+        if (a.var) a.var[off] = var;
+        if (a.std_mu) a.std_mu[off] = smu;
+        if (a.std_var) a.std_var[off] = svar;
+        if (a.ucb) a.ucb[off] = u;
+      }
+    }
+    if (valid && g == 0 && a.acq) a.acq[j] = acq;
+    if (a.topq > 0) {
+      long long gi = valid ? a.cand_offset + j : -1;
+      const double tv = __shfl(top_v, a.topq - 1, 64);
+      const long long ti = __shfl(top_i, a.topq - 1, 64);
+      const bool need = gi >= 0 && bo_better(acq, gi, tv, ti);
+      if (__ballot(need) != 0ull) {
+        // acquisition.py:137-139, exact f64 coordinates; lane group g checks points g, g+4, ...
+        bool hit = false;
+        for (int e = g; e < ne; e += 4) {
+          const double* r = es + (size_t)e * DIM;
+          bool eq = true;
+#pragma unroll
+          for (int k = 0; k < DIM; ++k) eq = eq && (r[k] == c[k]);
+          hit = hit || eq;
+        }
+        const unsigned long long hb = __ballot(hit);
+        if (((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull) gi = -1;
+      }
+      bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+    }
+  }
+  BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
+  if (a.topq > 0 && lane < a.topq) {
+    TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
+    dst[lane].v = top_v;
+    dst[lane].i = top_i;
+  }
+}
+
+template <int DIM>
+hipError_t launch_c32(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  auto k = cm32_predict_kernel<DIM>;
+  if (pl.lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)pl.lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(pl.grid), dim3(256), pl.lds, st, fa);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// one translation unit per padded dimension: bo_predict_d<D>.hip defines BO_PREDICT_DIM
+#ifdef BO_PREDICT_DIM
+#define BO_CAT_(a, b) a##b
+#define BO_CAT(a, b) BO_CAT_(a, b)
+namespace bo {
+hipError_t BO_CAT(launch_cm_d, BO_PREDICT_DIM)(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  return launch_cm<BO_PREDICT_DIM>(pl, fa, st);
+}
+hipError_t BO_CAT(launch_c32_d, BO_PREDICT_DIM)(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  return launch_c32<BO_PREDICT_DIM>(pl, fa, st);
+}
+}  // namespace bo
+#endif

@@ -15,11 +15,12 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
-VARIANT = os.environ.get("BO_BUILD_VARIANT", "")      # ablation builds: e.g. "NOEXP"
+VARIANT = os.environ.get("BO_BUILD_VARIANT", "")      # diagnostic builds: -DBO_ABL_<name>
 LIB = os.path.join(PKG, f"libbo_amd{('_' + VARIANT.lower().replace(',', '_')) if VARIANT else ''}.so")
 BUILD = os.path.join(HERE, "build" + (("_" + VARIANT.lower()) if VARIANT else ""))
-SOURCES = ["bo_predict.hip", "bo_fit.hip", "bo_select.hip", "bo_misc.hip", "bo_hvi.hip"]
-HEADERS = ["bo_common.h", os.path.join("..", "..", "include", "bo_amd.h")]
+SOURCES = ["bo_predict_d2.hip", "bo_predict_d4.hip", "bo_predict_d6.hip", "bo_predict_d8.hip",
+           "bo_predict.hip", "bo_fit.hip", "bo_select.hip", "bo_misc.hip", "bo_hvi.hip"]
+HEADERS = ["bo_common.h", "bo_predict_impl.h", os.path.join("..", "..", "include", "bo_amd.h")]
 ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", os.path.join(ROOT, "include")] + \
