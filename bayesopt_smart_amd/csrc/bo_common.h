@@ -78,7 +78,3 @@ __device__ __forceinline__ void bo_wave_topq_insert(double& lv, long long& li, d
   bo_wave_sort64(lv, li);
   if (lane >= q) { lv = -__builtin_inf(); li = -1; }
 }
-
-// Internal (not part of the C ABI): blocked Cholesky used by the fit and by the triangular
-// variance formulation of the fused predict kernel.  bo_fit.hip.
-int bo_internal_potrf(double* C, int n, int n_obj, int* d_status, hipStream_t s);

@@ -211,6 +211,31 @@ __device__ __forceinline__ double exp2_tab(double t, const double* tb) {
   return __builtin_ldexp(p * tb[ki & (kExpTab - 1)], ki >> 8);
 }
 
+#ifdef BO_ABL_OLDEXP
+// diagnostic build only: the round-1 table-free 2^t (range reduction to [-1/2, 1/2], degree 13)
+__device__ __forceinline__ double exp2_old(double t) {
+  const double x = fmax(t, -1100.0);
+  const double n = __builtin_rint(x);
+  const double r = x - n;
+  double p = 1.36914888539041241e-12;
+  p = __builtin_fma(p, r, 2.56784359934881958e-11);
+  p = __builtin_fma(p, r, 4.44553827187081007e-10);
+  p = __builtin_fma(p, r, 7.05491162080112088e-09);
+  p = __builtin_fma(p, r, 1.01780860092396960e-07);
+  p = __builtin_fma(p, r, 1.32154867901443053e-06);
+  p = __builtin_fma(p, r, 1.52527338040598377e-05);
+  p = __builtin_fma(p, r, 1.54035303933816061e-04);
+  p = __builtin_fma(p, r, 1.33335581464284411e-03);
+  p = __builtin_fma(p, r, 9.61812910762847688e-03);
+  p = __builtin_fma(p, r, 5.55041086648215762e-02);
+  p = __builtin_fma(p, r, 2.40226506959100694e-01);
+  p = __builtin_fma(p, r, 6.93147180559945286e-01);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_ldexp(p, (int)n);
+}
+#define exp2_tab(t, tb) exp2_old(t)
+#endif
+
 // Nested guards over the unrolled E-pair bodies: body E runs iff E < n, and is entered only
 // from body E - 1 (see chunk_step in cm_tiles).
 template <int E, int N>

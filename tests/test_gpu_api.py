@@ -48,6 +48,47 @@ def test_invert_k_matches_lapack(bo, n):
     assert np.abs(got - ref).max() <= 1e-13 * cond * scale
 
 
+def _sobol_problem(n, dim, n_obj, ls, seed):
+    from scipy.stats import qmc
+    x = qmc.Sobol(dim, scramble=True, seed=seed).random(n) * 300.0
+    y = np.stack([-((x[:, 0] - 150) ** 2) + 100, -((x[:, 1] - 150) ** 2) + 20,
+                  -((x[:, 2 % dim] - 5) ** 2) + 120][:n_obj], axis=1)
+    return x, y, y.mean(0), y.var(0), np.full(n_obj, ls)
+
+
+@pytest.mark.parametrize("n,dim,n_obj,ls", [(512, 2, 2, 20.0), (1024, 6, 3, 40.0), (2048, 6, 3, 40.0),
+                                            (3000, 6, 2, 40.0)])
+def test_invert_k_large_n_matches_lapack(bo, n, dim, n_obj, ls):
+    """The blocked-Cholesky inverse at the configs' N (C3 512, C4 1024, C5 2048) and beyond the
+    round-1 cap, against LAPACK's inv (numba_kernels.py:370-403)."""
+    import torch
+    x, y, pm, pv, lsv = _sobol_problem(n, dim, n_obj, ls, n)
+    km = torch.zeros((n_obj, n, n), dtype=torch.float64, device="cuda")
+    bo.kernels.update_k(km, torch.tensor(x, device="cuda"), 0, n, pv, lsv)
+    got = bo.kernels.invert_k(n, km).cpu().numpy()
+    k_h = km.cpu().numpy()
+    ref = O.invert_k(n, k_h)
+    for o in range(n_obj):
+        cond = np.linalg.cond(k_h[o] + 1e-6 * np.eye(n)) if n <= 2048 else 1e6
+        scale = np.abs(ref[o]).max()
+        assert np.abs(got[o] - ref[o]).max() <= 1e-13 * cond * scale, (o, cond)
+
+
+@pytest.mark.parametrize("n,dim,n_obj,ls", [(512, 2, 2, 20.0), (1024, 6, 3, 40.0), (2048, 6, 3, 40.0)])
+def test_compute_mll_large_n_matches_reference_algorithm(bo, n, dim, n_obj, ls):
+    """compute_mll at the configs' N against the oracle (LAPACK cholesky + solves,
+    numba_kernels.py:152-235), and the caller's kernel_matrix rebuilt as the reference does."""
+    import torch
+    x, y, pm, pv, lsv = _sobol_problem(n, dim, n_obj, ls, n + 1)
+    km = torch.zeros((n_obj, n, n), dtype=torch.float64, device="cuda")
+    v = bo.kernels.compute_mll(torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda"), km, pm, pv,
+                               lsv, n)
+    km_h = np.zeros((n_obj, n, n))
+    ref = O.compute_mll(x, y, km_h, pm, pv, lsv, n)
+    assert v == pytest.approx(ref, rel=1e-9)
+    np.testing.assert_allclose(km.cpu().numpy(), km_h, rtol=1e-14, atol=0)
+
+
 def test_invert_k_pivoting_and_singular(bo):
     # a matrix that needs row interchanges (zero leading pivot after the jitter is tiny)
     a = np.array([[[0.0, 2.0, 1.0], [3.0, 1.0, 0.0], [1.0, 0.0, 4.0]]])
