@@ -21,7 +21,8 @@ MAX_DIM = 8
 MAX_TOPQ = 48
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_WORKSPACE, ERR_HIP, ERR_NOT_PD, ERR_SINGULAR = range(7)
-CAND_I64, CAND_F64, CAND_GRID = 0, 1, 2
+CAND_I64, CAND_F64, CAND_GRID, CAND_SOBOL = 0, 1, 2, 3
+ABI_VERSION = 2
 MODE_AUTO, MODE_DENSE, MODE_NO_SEPARABLE = 0, 1, 2
 
 c_dbl_p = C.POINTER(C.c_double)
@@ -52,6 +53,13 @@ class PredictDesc(C.Structure):
         ("topq", C.c_int32), ("reserved1", C.c_int32),
         ("top_val", c_vp), ("top_idx", c_vp),
     ]
+
+
+class SobolDesc(C.Structure):
+    """Mirror of bo_sobol_desc (include/bo_amd.h)."""
+
+    _fields_ = [("bits", C.c_int32), ("reserved", C.c_int32),
+                ("lo", C.c_double * MAX_DIM), ("scale", C.c_double * MAX_DIM)]
 
 
 _SIGS = {
@@ -87,6 +95,9 @@ _SIGS = {
                                  C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, c_vp, C.c_size_t,
                                  c_vp]),
     "bo_compute_mll_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
+    "bo_sobol_points": (C.c_int, [C.POINTER(SobolDesc), C.c_int32, C.POINTER(C.c_int64), C.c_int64,
+                                  c_dbl_p]),
+    "bo_sobol_direction_numbers": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_uint32)]),
     "bo_selftest_mfma_f64": (C.c_int, [c_vp, c_vp, c_vp, c_vp]),
     "bo_selftest_mfma_f32": (C.c_int, [c_vp, c_vp, c_vp, c_vp]),
     "bo_profile_start": (C.c_int, [C.c_int]),
@@ -109,7 +120,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.bo_abi_version() != 1:
+    if lib.bo_abi_version() != ABI_VERSION:
         raise BoNativeError(ERR_UNSUPPORTED, "ABI version mismatch")
     _lib = lib
     return lib

@@ -75,9 +75,7 @@ def select_indices(acquisition_values, cands, evaluated_points, batch_size, dev=
         sh = (C_i64 * 8)(*(list(cands.shape or []) + [1] * (8 - len(cands.shape or []))))
         nbytes = lib.bo_select_topq_workspace_size(cands.n, q)
         ws = Workspace.get(nbytes, dev)
-        _lib.check(lib.bo_select_topq(acq.ptr, cands.n, cands.kind_code,
-                                      cands.tensor.data_ptr() if cands.tensor is not None else None,
-                                      lo, sh, cands.dim, 0, ex.data_ptr() if ex.numel() else None,
+        _lib.check(lib.bo_select_topq(acq.ptr, cands.n, cands.kind_code, cands.cand_arg, lo, sh, cands.dim, 0, ex.data_ptr() if ex.numel() else None,
                                       ex.shape[0], q, tv.data_ptr(), ti.data_ptr(), ws.data_ptr(),
                                       ws.numel(), stream_handle(dev)), "bo_select_topq")
         got = [int(i) for i in ti.cpu().numpy() if i >= 0]

@@ -78,3 +78,31 @@ __device__ __forceinline__ void bo_wave_topq_insert(double& lv, long long& li, d
   bo_wave_sort64(lv, li);
   if (lane >= q) { lv = -__builtin_inf(); li = -1; }
 }
+
+// ---------------------------------------------------------------------------------------
+// Sobol candidates (BO_CAND_SOBOL): direction numbers (host) and one coordinate (device).
+// ---------------------------------------------------------------------------------------
+struct SobolArgs {
+  unsigned int v[BO_MAX_DIM][32];   // direction numbers scaled to `bits`
+  double lo[BO_MAX_DIM], scale[BO_MAX_DIM];
+  int bits;
+};
+
+// Direction numbers of scipy.stats.qmc.Sobol (Joe & Kuo's table, first BO_MAX_DIM dimensions:
+// primitive polynomials and initial m_j), built as Bratley & Fox's recurrence; bo_misc.hip.
+int bo_sobol_fill(SobolArgs* s, int dim, const bo_sobol_desc* d);
+
+// coordinate k of Sobol point i: lo + (x / 2^bits) * scale, x = XOR_{bits j of gray(i)} v[k][j]
+__host__ __device__ inline double bo_sobol_coord(const SobolArgs& s, int k, unsigned long long i) {
+  const unsigned long long g = i ^ (i >> 1);
+  unsigned int x = 0;
+  for (int b = 0; b < s.bits; ++b)
+    if ((g >> b) & 1ull) x ^= s.v[k][b];
+  const double u = ldexp((double)x, -s.bits);          // exact
+#ifdef __HIP_DEVICE_COMPILE__
+  return __dadd_rn(s.lo[k], __dmul_rn(u, s.scale[k]));  // numpy: lo + sample * scale, unfused
+#else
+  volatile double t = u * s.scale[k];
+  return s.lo[k] + t;
+#endif
+}

@@ -257,17 +257,21 @@ __global__ void prep_rows_kernel(double* __restrict__ xpad, double* __restrict__
   if (f < n && ext) atomicMax(ext, (unsigned long long)__double_as_longlong(s));
 }
 
-// ext[1] = max over the call's explicit candidates of |c - z|^2 (z = x_0), for the dot-form gate.
-__global__ void cand_extent_kernel(unsigned long long* __restrict__ ext, const void* __restrict__ cand,
-                                   int kind, long long n_cand, int dim, const double* __restrict__ x) {
+// ext[1] = max over the call's candidates (explicit or Sobol) of |c - z|^2 (z = x_0, the first
+// padded training row), for the dot-form gate.
+__global__ void cand_extent_kernel(unsigned long long* __restrict__ ext, const FusedArgs a) {
+  double z[BO_MAX_DIM];
+#pragma unroll
+  for (int k = 0; k < BO_MAX_DIM; ++k) z[k] = k < a.dim ? a.xpad[k] : 0.0;
   double m = 0.0;
-  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < n_cand;
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < a.n_cand;
        j += (long long)gridDim.x * blockDim.x) {
+    double c[BO_MAX_DIM];
+    load_candidate<BO_MAX_DIM>(a, j, true, c);
     double s = 0.0;
-    for (int k = 0; k < dim; ++k) {
-      const double c = kind == BO_CAND_I64 ? (double)((const long long*)cand)[j * dim + k]
-                                           : ((const double*)cand)[j * dim + k];
-      const double d = c - x[k];
+#pragma unroll
+    for (int k = 0; k < BO_MAX_DIM; ++k) {
+      const double d = c[k] - z[k];
       s = __builtin_fma(d, d, s);
     }
     m = (s > m || s != s) ? s : m;
@@ -280,9 +284,6 @@ __global__ void cand_extent_kernel(unsigned long long* __restrict__ ext, const v
   if ((threadIdx.x & 63) == 0) atomicMax(ext + 1, (unsigned long long)__double_as_longlong(m));
 }
 
-// Pack K^-1 into the MFMA fragment order of kmem_predict_kernel (the materialised-K* path),
-// zero padded.  Element (panel, ep, pair, which, lane) holds
-// W[16E + (l&15)][4s + (l>>4)] and the same at s+1 (E = 2ep + which, s = panel*ns_panel + 2*pair).
 __global__ void pack_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
                             int n, int n_pad, int ns_panel, int n_obj) {
   const long long per_obj = (long long)n_pad * n_pad / 2;
@@ -520,7 +521,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   if (!d || d->n_obj < 1 || d->n_obj > BO_MAX_OBJ || d->dim < 1 || d->dim > BO_MAX_DIM)
     return BO_ERR_ARG;
   if (d->n_train < 1 || d->n_cand < 0 || d->topq < 0 || d->topq > BO_MAX_TOPQ) return BO_ERR_ARG;
-  if (d->cand_kind < 0 || d->cand_kind > 2) return BO_ERR_ARG;
+  if (d->cand_kind < 0 || d->cand_kind > BO_CAND_SOBOL) return BO_ERR_ARG;
   if (d->mode & ~(BO_PREDICT_DENSE | BO_PREDICT_NO_SEPARABLE | BO_PREDICT_FP32)) return BO_ERR_ARG;
   if (d->excl_points && d->n_excl < 0) return BO_ERR_ARG;
   const long long n = d->n_train;
@@ -712,6 +713,13 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     if (d->cand_offset < 0 || d->cand_offset + d->n_cand > total) return BO_ERR_ARG;
   }
   fa.cand = d->cand;
+  if (d->cand_kind == BO_CAND_SOBOL) {
+    if (!d->cand) return BO_ERR_ARG;
+    st = bo_sobol_fill(&fa.sob, d->dim, (const bo_sobol_desc*)d->cand);
+    if (st != BO_OK) return st;
+    if (d->cand_offset < 0 || (unsigned long long)(d->cand_offset + d->n_cand) > (1ull << fa.sob.bits))
+      return BO_ERR_ARG;
+  }
   fa.xpad = xpad;
   fa.xc = xc;
   fa.sqg = sq;
@@ -779,7 +787,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
       if (pl.cm && fa.upper && pl.dotx && d->n_cand > 0) {
         const long long nb = (d->n_cand + 255) / 256;
         hipLaunchKernelGGL(cand_extent_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(256), 0, s,
-                           ext, d->cand, d->cand_kind, (long long)d->n_cand, d->dim, d->x_train);
+                           ext, fa);
         BO_CHECK_HIP(hipGetLastError());
       }
     }

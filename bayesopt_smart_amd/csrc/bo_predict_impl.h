@@ -64,6 +64,7 @@ struct FusedArgs {
   int dotx;                              // explicit candidates, upper form: dot-form exponent allowed
   int off_sq;                            // LDS offset (doubles) of |xc_f|^2 (LDS-resident rows)
   int off_exp;                           // LDS offset (doubles) of the 2^(j/256) table
+  SobolArgs sob;                         // kind BO_CAND_SOBOL: direction numbers, lo, scale
 };
 
 // Host-side plan of one bo_predict_acquire call (bo_predict.hip: make_plan).
@@ -129,6 +130,12 @@ __device__ __forceinline__ void load_candidate(const FusedArgs& a, long long j, 
 #pragma unroll
     for (int k = 0; k < DIM; ++k)
       if (k < a.dim) c[k] = (double)p[k];
+  } else if (a.cand_kind == BO_CAND_SOBOL) {
+    // generated from the global index (scipy.stats.qmc.Sobol(scramble=False), bit-identical)
+    const unsigned long long gi = (unsigned long long)(a.cand_offset + j);
+#pragma unroll
+    for (int k = 0; k < DIM; ++k)
+      if (k < a.dim) c[k] = bo_sobol_coord(a.sob, k, gi);
   } else {
     const double* p = (const double*)a.cand + j * a.dim;
 #pragma unroll
@@ -714,6 +721,12 @@ __global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
     double nl = 0.0;
     for (int o = 0; o < a.n_obj; ++o) nl = fmax(nl, fabs(a.nhl[o] * 1.4426950408889634));
     dotx = nl * (rx + rc) <= bo::kDotxLimit;
+#ifdef BO_ABL_FORCEDOTX
+    dotx = true;
+#endif
+#ifdef BO_ABL_NODOTX
+    dotx = false;
+#endif
   }
   __syncthreads();
   if constexpr (GRID && !GROWS) {

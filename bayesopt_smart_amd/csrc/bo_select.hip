@@ -108,6 +108,7 @@ struct SelArgs {
   const double* excl;
   const uint32_t* bitmap;   // grid kind: bit j set iff local candidate j is excluded (else NULL)
   TopEntry* partial;
+  SobolArgs sob;            // kind BO_CAND_SOBOL
 };
 
 // Grid kind: mark the evaluated points that lie on this shard of the grid in a bitmap over the
@@ -129,6 +130,7 @@ __global__ void excl_bitmap_kernel(uint32_t* __restrict__ bm, SelArgs a) {
 __device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int k) {
   if (a.kind == BO_CAND_I64) return (double)((const long long*)a.cand)[j * a.dim + k];
   if (a.kind == BO_CAND_F64) return ((const double*)a.cand)[j * a.dim + k];
+  if (a.kind == BO_CAND_SOBOL) return bo_sobol_coord(a.sob, k, (unsigned long long)(a.cand_offset + j));
   long long gi = a.cand_offset + j;
   for (int t = a.dim - 1; t > k; --t) gi /= a.grid_shape[t];
   return (double)(a.grid_lo[k] + gi % a.grid_shape[k]);
@@ -356,7 +358,7 @@ int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* 
                    int64_t cand_offset, const double* excl, int64_t n_excl, int32_t topq,
                    double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes, void* stream) {
   if (!acq || topq < 1 || topq > BO_MAX_TOPQ || dim < 1 || dim > BO_MAX_DIM || n_cand < 0 ||
-      !top_val || !top_idx || (n_excl > 0 && !excl) || kind < 0 || kind > 2)
+      !top_val || !top_idx || (n_excl > 0 && !excl) || kind < 0 || kind > BO_CAND_SOBOL)
     return BO_ERR_ARG;
   if (kind != BO_CAND_GRID && !cand) return BO_ERR_ARG;
   if (kind == BO_CAND_GRID && (!grid_lo || !grid_shape)) return BO_ERR_ARG;
@@ -372,6 +374,11 @@ int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* 
   a.n_excl = (int)n_excl;
   a.topq = topq;
   a.cand = cand;
+  if (kind == BO_CAND_SOBOL) {            // `cand` is a host bo_sobol_desc*
+    const int st = bo_sobol_fill(&a.sob, dim, (const bo_sobol_desc*)cand);
+    if (st != BO_OK) return st;
+    a.cand = nullptr;
+  }
   for (int k = 0; k < BO_MAX_DIM; ++k) a.grid_shape[k] = 1;
   if (kind == BO_CAND_GRID)
     for (int k = 0; k < dim; ++k) {

@@ -28,8 +28,10 @@ class CandidateSet:
 
     kind ``grid``: the reference's integer 'ij' meshgrid (bayesian_optimization.py:338-340),
     generated on the device from the linear index (no candidate array in HBM);
-    kind ``i64``/``f64``: an explicit [M, d] device array (the reference's input_space, or
-    e.g. a Sobol set).
+    kind ``sobol``: the unscrambled Sobol sequence of scipy.stats.qmc.Sobol(d, scramble=False)
+    mapped to lo + u * scale, generated on the device from the index (bit-identical to scipy;
+    each candidate shard generates its own index range);
+    kind ``i64``/``f64``: an explicit [M, d] device array (the reference's input_space).
     """
 
     kind: str
@@ -38,6 +40,7 @@ class CandidateSet:
     tensor: Optional[torch.Tensor] = None
     lo: Optional[Sequence[int]] = None
     shape: Optional[Sequence[int]] = None
+    sobol: Optional[object] = None          # _lib.SobolDesc (kind "sobol")
 
     @staticmethod
     def grid(bounds):
@@ -45,6 +48,21 @@ class CandidateSet:
         shape = [int(b[1]) - int(b[0]) for b in bounds]
         n = int(np.prod(shape, dtype=np.int64))
         return CandidateSet("grid", n, len(bounds), lo=lo, shape=shape)
+
+    @staticmethod
+    def sobol_set(dim, n, lo=0.0, scale=1.0, bits=30):
+        """Points 0 .. n-1 of scipy.stats.qmc.Sobol(dim, scramble=False, bits=bits).random(n),
+        as lo + u * scale per dimension (scalars or sequences)."""
+        if not 1 <= dim <= _lib.MAX_DIM or not 1 <= bits <= 32 or n > (1 << bits):
+            raise ValueError("Sobol set needs 1 <= dim <= 8, 1 <= bits <= 32 and n <= 2^bits")
+        d = _lib.SobolDesc()
+        d.bits = bits
+        lo = np.broadcast_to(np.asarray(lo, dtype=np.float64), (dim,))
+        scale = np.broadcast_to(np.asarray(scale, dtype=np.float64), (dim,))
+        for k in range(dim):
+            d.lo[k] = float(lo[k])
+            d.scale[k] = float(scale[k])
+        return CandidateSet("sobol", int(n), int(dim), sobol=d)
 
     @staticmethod
     def explicit(points, device=None):
@@ -62,11 +80,27 @@ class CandidateSet:
 
     @property
     def kind_code(self):
-        return {"i64": _lib.CAND_I64, "f64": _lib.CAND_F64, "grid": _lib.CAND_GRID}[self.kind]
+        return {"i64": _lib.CAND_I64, "f64": _lib.CAND_F64, "grid": _lib.CAND_GRID,
+                "sobol": _lib.CAND_SOBOL}[self.kind]
+
+    @property
+    def cand_arg(self):
+        """The `cand` argument of the ABI calls: device array pointer, or the host Sobol desc."""
+        import ctypes
+        if self.kind == "sobol":
+            return ctypes.cast(ctypes.pointer(self.sobol), ctypes.c_void_p).value
+        return None if self.tensor is None else self.tensor.data_ptr()
 
     def points(self, idx):
         """Coordinates of global candidate indices (numpy [k, d]; int64 for grid/i64)."""
-        idx = np.asarray(idx, dtype=np.int64)
+        idx = np.ascontiguousarray(idx, dtype=np.int64).ravel()
+        if self.kind == "sobol":
+            import ctypes
+            out = np.empty((idx.size, self.dim), dtype=np.float64)
+            _lib.check(_lib.load().bo_sobol_points(
+                ctypes.byref(self.sobol), self.dim, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                idx.size, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "bo_sobol_points")
+            return out
         if self.kind == "grid":
             out = np.empty((idx.size, self.dim), dtype=np.int64)
             rem = idx.copy()
@@ -77,7 +111,9 @@ class CandidateSet:
         return self.tensor[torch.as_tensor(idx, device=self.tensor.device)].cpu().numpy()
 
     def materialize(self, device=None):
-        """Explicit int64 [M, d] tensor of a grid (the reference's input_space)."""
+        """Explicit [M, d] tensor: int64 for a grid (the reference's input_space), f64 Sobol."""
+        if self.kind == "sobol":
+            return torch.as_tensor(self.points(np.arange(self.n)), device=require_device(device))
         if self.kind != "grid":
             return self.tensor
         dev = require_device(device)
@@ -110,6 +146,8 @@ def _fill_desc(x_train, y_train, kinv, cands, pm, pv, ls, betas, offset, count, 
             d.grid_lo[k] = cands.lo[k]
             d.grid_shape[k] = cands.shape[k]
         d.cand = None
+    elif cands.kind == "sobol":
+        d.cand = cands.cand_arg                  # host bo_sobol_desc, read during the call
     else:
         # explicit candidates: the call sees rows [offset, offset + count)
         d.cand = cands.tensor.data_ptr() + offset * cands.dim * cands.tensor.element_size()

@@ -108,7 +108,7 @@ def _kinv(x, pv, ls):
 
 def make_config_problem(cfg, world):
     """Seeded inputs of SURVEY.md §8d.  Returns (x, y, pm, pv, ls, betas, kinv, cand) where cand
-    is ('grid', rows, side) or ('sobol', points [M, d] f64)."""
+    is ('grid', rows, side) or ('sobol', CandidateSet of kind sobol)."""
     rng = np.random.default_rng(0)
     if cfg["kind"] == "grid":
         side = cfg["side"]
@@ -118,11 +118,14 @@ def make_config_problem(cfg, world):
         y = toy_function(x)
         cand = ("grid", rows, side)
     else:
-        from scipy.stats import qmc
-        pts = qmc.Sobol(cfg["dim"], scramble=False).random(cfg["m"]) * 300.0
-        x = pts[rng.choice(cfg["m"], size=cfg["n_train"], replace=False)]
+        # the unscrambled Sobol set (scipy.stats.qmc.Sobol(6, scramble=False) * 300), generated by
+        # the library from the index -- on the device inside the kernel, on the host here for
+        # the training points (bit-identical to scipy, tests/test_sobol.py)
+        from bayesopt_smart_amd.predict import CandidateSet
+        cs = CandidateSet.sobol_set(cfg["dim"], cfg["m"], scale=300.0)
+        x = cs.points(rng.choice(cfg["m"], size=cfg["n_train"], replace=False))
         y = toy_function_3d(x)
-        cand = ("sobol", pts)
+        cand = ("sobol", cs)
     pm, pv = y.mean(0), y.var(0)                               # compute_prior_mean / _variance
     ls = np.full(cfg["n_obj"], cfg["ls"])
     betas = np.full(cfg["n_obj"], BETA)
@@ -355,11 +358,12 @@ def main():
         offset = rank * per_rank
         total = world * per_rank
     else:
-        # strong scaling: the fixed Sobol set split into P balanced contiguous index ranges
-        m = cand[1].shape[0]
+        # strong scaling: the fixed Sobol set split into P balanced contiguous index ranges; each
+        # rank's kernel generates its own range from the index (no candidate array anywhere)
+        cands = cand[1]
+        m = cands.n
         offset, per_rank = shard_range(m, rank, world)
         total = m
-        cands = bo.CandidateSet.explicit(cand[1], device=dev)
     xd = torch.tensor(x, device=dev)
     yd = torch.tensor(y, device=dev)
     kd = torch.tensor(kinv, device=dev)
@@ -402,7 +406,7 @@ def main():
             hvi_ev.append((e0, e1))
             bo._lib.check(lib.bo_select_topq(
                 out["acq"].data_ptr(), per_rank, cands.kind_code,
-                cands.tensor[offset:].data_ptr() if cands.tensor is not None else None, glo, gsh,
+                (cands.tensor[offset:].data_ptr() if cands.kind in ("i64", "f64") else cands.cand_arg), glo, gsh,
                 cands.dim, offset, exd.data_ptr(), exd.shape[0], q, rec.data_ptr(),
                 rec.data_ptr() + 8 * q, sel_ws.data_ptr(), sel_ws.numel(), strm), "select")
 
@@ -514,7 +518,7 @@ def main():
                 label = f"{args.config} grid"
             else:
                 def points(lo, hi):
-                    return cand[1][lo:hi]
+                    return cands.points(np.arange(lo, hi))
                 label = f"{args.config} Sobol set"
             cb, cpu_acq, cpu_sel = cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q,
                                                 max_cand=per_rank)
@@ -524,10 +528,7 @@ def main():
             gpu_acq = out["acq"][:done].cpu().numpy()
             res["acq_max_err_vs_cpu"] = float(np.max(np.abs(gpu_acq - cpu_acq) / np.maximum(1.0, np.abs(cpu_acq))))
             if done == per_rank:
-                xs = {tuple(r) for r in x}
-                pts = points(0, done)
-                excluded = np.fromiter((tuple(p) in xs for p in pts), dtype=bool, count=done) \
-                    if cand[0] != "grid" else _grid_excluded(x, side, done)
+                excluded = _rows_in(points(0, done), x) if cand[0] != "grid" else _grid_excluded(x, side, done)
                 res["selection_matches_cpu"] = selection_check(sel[1], cpu_acq, excluded, q)
                 res["cpu_selected"] = [int(i) for i in cpu_sel]
             else:
@@ -535,6 +536,12 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _rows_in(pts, x):
+    """Mask of the rows of pts equal (all coordinates) to some row of x."""
+    v = lambda a: np.ascontiguousarray(a, dtype=np.float64).view(np.dtype((np.void, 8 * a.shape[1]))).ravel()  # noqa: E731
+    return np.isin(v(pts), v(x))
 
 
 def _grid_excluded(x, side, m):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 1
+#define BO_ABI_VERSION 2
 #define BO_MAX_OBJ 8      /* objectives per call                              */
 #define BO_MAX_DIM 8      /* input dimensions                                 */
 #define BO_MAX_TOPQ 48    /* batch size of the fused top-q selection          */
@@ -43,8 +43,30 @@ typedef enum bo_status {
 typedef enum bo_cand_kind {
   BO_CAND_I64 = 0,   /* explicit candidates, int64 [n_cand][dim] (the reference's input_space) */
   BO_CAND_F64 = 1,   /* explicit candidates, f64 [n_cand][dim] (e.g. a Sobol set)            */
-  BO_CAND_GRID = 2   /* implicit 'ij' integer grid: bayesian_optimization.py:338-340           */
+  BO_CAND_GRID = 2,  /* implicit 'ij' integer grid: bayesian_optimization.py:338-340           */
+  BO_CAND_SOBOL = 3  /* implicit unscrambled Sobol sequence, generated on the device from the
+                        global index: point i of scipy.stats.qmc.Sobol(dim, scramble=False,
+                        bits) mapped to lo + u * scale (bit-identical; `cand` is a HOST
+                        bo_sobol_desc*, read during the call).  A candidate-shard generates its
+                        own index range: no candidate array exists in HBM or crosses PCIe.   */
 } bo_cand_kind;
+
+/* Parameters of kind BO_CAND_SOBOL: coordinate k of point i is lo[k] + u_k(i) * scale[k]
+ * (multiply, then add: numpy's `lo + sample * (hi - lo)`), u_k(i) = x_k(i) / 2^bits with
+ * x_k(i) = XOR of the direction numbers v_kj over the set bits j of gray(i) = i ^ (i >> 1)
+ * (Joe-Kuo direction numbers, the table scipy ships).  bits in [1, 32]; i < 2^bits. */
+typedef struct bo_sobol_desc {
+  int32_t bits;
+  int32_t reserved;
+  double lo[BO_MAX_DIM];
+  double scale[BO_MAX_DIM];
+} bo_sobol_desc;
+
+/* HOST (no device, synchronous): coordinates out[t][k] (t < n, k < dim) of the Sobol points with
+ * global indices idx[t], bit-identical to the device generator; the direction numbers
+ * v[dim][bits] (uint32, row-major). */
+int bo_sobol_points(const bo_sobol_desc* s, int32_t dim, const int64_t* idx, int64_t n, double* out);
+int bo_sobol_direction_numbers(int32_t dim, int32_t bits, uint32_t* out);
 
 int bo_abi_version(void);
 const char* bo_status_string(int status);
@@ -94,7 +116,7 @@ typedef struct bo_predict_desc {
   int64_t ld_k;
   int32_t cand_kind;          /* bo_cand_kind                                                 */
   int32_t mode;               /* bo_predict_mode                                              */
-  const void* cand;           /* device [n_cand][dim] (kinds I64/F64)                         */
+  const void* cand;           /* device [n_cand][dim] (kinds I64/F64); host bo_sobol_desc* (SOBOL) */
   int64_t n_cand;             /* candidates scored by this call                               */
   int64_t cand_offset;        /* global index of this call's first candidate                  */
   int64_t grid_lo[BO_MAX_DIM];     /* kind GRID: lower bound of each axis                    */

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_status_strings_and_version():
     from bayesopt_smart_amd import _lib
     lib = _lib.load()
-    assert lib.bo_abi_version() == 1
+    assert lib.bo_abi_version() == _lib.ABI_VERSION == 2
     assert lib.bo_status_string(_lib.ERR_NOT_PD) == b"Matrix is not positive definite"
     with pytest.raises(np.linalg.LinAlgError):
         _lib.check(_lib.ERR_SINGULAR, "x")
@@ -57,6 +57,22 @@ def test_desc_layout_matches_header():
     assert vals[0] == ctypes.sizeof(_lib.PredictDesc)
     for f, off in zip(fields, vals[1:]):
         assert getattr(_lib.PredictDesc, f).offset == off, f
+    # bo_sobol_desc likewise
+    sf = [f for f, _ in _lib.SobolDesc._fields_]
+    prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"bo_amd.h\"\nint main(){\n"
+    prog += 'printf("%zu\\n", sizeof(bo_sobol_desc));\n'
+    for f in sf:
+        prog += f'printf("%zu\\n", offsetof(bo_sobol_desc, {f}));\n'
+    prog += "return 0;}\n"
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        vals = [int(v) for v in subprocess.check_output([exe]).split()]
+    assert vals[0] == ctypes.sizeof(_lib.SobolDesc)
+    for f, off in zip(sf, vals[1:]):
+        assert getattr(_lib.SobolDesc, f).offset == off, f
 
 
 def test_workspace_size_queries():

@@ -105,12 +105,19 @@ def test_c4_c5_sobol_6d_3obj(bo, n, m_full, q, mode):
     check_topq(out["top_idx"], ref["acq"], excluded_rows(cand, x), q)
     if mode == "dense":
         return
-    # the shard partition (distributed.shard_range over 4 ranks) reproduces the single call
+    # the device Sobol generator (kind sobol: the kernel generates each point from its index)
+    # reproduces the explicit scipy set bit for bit, outputs and selection included
+    sob = bo.predict.CandidateSet.sobol_set(6, m_full, scale=300.0)
+    o = run(bo, d, sob, q, mode)
+    for k in ("mu", "var", "acq", "top_idx"):
+        np.testing.assert_array_equal(o[k], out[k], err_msg=k)
+    # the shard partition (distributed.shard_range over 4 ranks, each generating its own Sobol
+    # index range) reproduces the single call
     from bayesopt_smart_amd.distributed import shard_range
     vals, idxs = [], []
     for r in range(4):
         off, cnt = shard_range(m_full, r, 4)
-        o = run(bo, d, cands, q, outputs=("acq",), offset=off, count=cnt)
+        o = run(bo, d, sob, q, outputs=("acq",), offset=off, count=cnt)
         np.testing.assert_array_equal(o["acq"], out["acq"][off:off + cnt])
         vals.append(o["top_val"])
         idxs.append(o["top_idx"])
