@@ -144,22 +144,27 @@ __global__ __launch_bounds__(256, 1) void kmem_predict_kernel(const FusedArgs a)
 // E = 2ep + 1, 64 lanes x 16 B each: {W[16E + (l&15)][4s + (l>>4)], same at s+1}.
 //   dense: W = K^-1 (leading dim ld);
 //   upper: W[e][f] = (K^-1[e][f] + K^-1[f][e]) / 2 for f > e, K^-1[e][e] / 2 for f == e, else 0.
-__device__ __forceinline__ long long cm_group_blocks(int nch, int e0, int upper) {
+__host__ __device__ inline long long cm_group_blocks(int nch, int e0, int upper) {
   const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
   if (!upper) return (long long)nch * eN;
   // chunks e0 .. e0+eN-2 hold 1 .. eN-1 blocks, the nch - e0 - eN + 1 later ones eN each
   return (long long)(eN - 1) * eN / 2 + (long long)(nch - e0 - eN + 1) * eN;
 }
 
-__global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
-                               int upper, int n, int n_pad, int n_obj) {
-  const int nch = n_pad / 32;
+__host__ __device__ inline long long cm_blocks(int nch, int upper) {
   long long blocks = 0;
   for (int e0 = 0; e0 < nch; e0 += kCMaxEp) blocks += cm_group_blocks(nch, e0, upper);
-  const long long per_obj = blocks * 512;                     // d2 entries (4 pairs x 2 x 64)
-  const long long stride_obj = (long long)n_pad * n_pad / 2;  // d2 entries reserved per objective
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per_obj * n_obj;
-       t += (long long)gridDim.x * blockDim.x) {
+  return blocks;
+}
+
+// The objectives' streams are contiguous (objective o starts at pair 4 o blocks), so that the
+// kernel's W ring runs on from one objective into the next without a restart.
+__device__ void pack_cm_range(long long t0, long long stride, d2* __restrict__ out,
+                              const double* __restrict__ kinv, long long ld, int upper, int n,
+                              int n_pad, int n_obj) {
+  const int nch = n_pad / 32;
+  const long long per_obj = cm_blocks(nch, upper) * 512;      // d2 entries (4 pairs x 2 x 64)
+  for (long long t = t0; t < per_obj * n_obj; t += stride) {
     const int o = (int)(t / per_obj);
     long long r = t - (long long)o * per_obj;
     const int lane = (int)(r & 63); r >>= 6;
@@ -210,88 +215,22 @@ __global__ void pack_cm_kernel(d2* __restrict__ out, const double* __restrict__ 
     d2 v;
     v.x = w(row, col0);
     v.y = w(row, col1);
-    out[(long long)o * stride_obj + (t - (long long)o * per_obj)] = v;
+    out[t] = v;
   }
 }
 
-// Separable-K* precondition on the training rows: last coordinate integral and inside the
-// grid's last axis [lo, lo + S - 1] (else *flag = 1 and the kernel keeps the exp path).
-__global__ void sep_check_kernel(const double* __restrict__ x, int n, int dim, long long lo, int S,
-                                 int* __restrict__ flag) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n) return;
-  const double v = x[(long long)f * dim + dim - 1];
-  const bool ok = v == __builtin_rint(v) && v >= (double)lo && v <= (double)(lo + S - 1);
-  if (!ok) atomicOr(flag, 1);
-}
 
-// Evaluated points padded to [rows][DIM]: coordinates beyond `dim` are 0.
-__global__ void pad_points_kernel(double* __restrict__ out, const double* __restrict__ in,
-                                  int rows, int rows_pad, int dim, int DIM, double fill) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= rows_pad * DIM) return;
-  const int r = t / DIM, k = t - r * DIM;
-  out[t] = r < rows ? (k < dim ? in[r * dim + k] : 0.0) : fill;
-}
-
-// Training rows, one thread per padded row f < n_pad:
-//   xpad[f] = x_f (coordinates beyond `dim` 0; padded rows 1e200 so that every K* of theirs is
-//             exactly 0), the original coordinates (grid row pass, exact exclusion tests);
-//   xc[f]   = x_f - z with the centre z = x_0 (distances are translation invariant);
-//   sq[f]   = |xc_f|^2 (inf for padded rows), and ext[0] = max_{f < n} sq[f] (integer max of the
-//             non-negative doubles' bit patterns) for the dot-form gate.
-__global__ void prep_rows_kernel(double* __restrict__ xpad, double* __restrict__ xc,
-                                 double* __restrict__ sq, unsigned long long* __restrict__ ext,
-                                 const double* __restrict__ x, int n, int n_pad, int dim, int DIM) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n_pad) return;
-  double s = 0.0;
-  for (int k = 0; k < DIM; ++k) {
-    const double v = f < n ? (k < dim ? x[(long long)f * dim + k] : 0.0) : 1e200;
-    const double c = f < n ? v - (k < dim ? x[k] : 0.0) : 1e200;
-    xpad[(long long)f * DIM + k] = v;
-    xc[(long long)f * DIM + k] = c;
-    s = __builtin_fma(c, c, s);
-  }
-  sq[f] = s;
-  if (f < n && ext) atomicMax(ext, (unsigned long long)__double_as_longlong(s));
-}
-
-// ext[1] = max over the call's candidates (explicit or Sobol) of |c - z|^2 (z = x_0, the first
-// padded training row), for the dot-form gate.
-__global__ void cand_extent_kernel(unsigned long long* __restrict__ ext, const FusedArgs a) {
-  double z[BO_MAX_DIM];
-#pragma unroll
-  for (int k = 0; k < BO_MAX_DIM; ++k) z[k] = k < a.dim ? a.xpad[k] : 0.0;
-  double m = 0.0;
-  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < a.n_cand;
-       j += (long long)gridDim.x * blockDim.x) {
-    double c[BO_MAX_DIM];
-    load_candidate<BO_MAX_DIM>(a, j, true, c);
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < BO_MAX_DIM; ++k) {
-      const double d = c[k] - z[k];
-      s = __builtin_fma(d, d, s);
-    }
-    m = (s > m || s != s) ? s : m;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double v = __shfl_xor(m, o, 64);
-    m = (v > m || v != v) ? v : m;
-  }
-  if ((threadIdx.x & 63) == 0) atomicMax(ext + 1, (unsigned long long)__double_as_longlong(m));
-}
-
-__global__ void pack_kernel(d2* __restrict__ out, const double* __restrict__ kinv, long long ld,
-                            int n, int n_pad, int ns_panel, int n_obj) {
+// Pack K^-1 into the MFMA fragment order of kmem_predict_kernel (the materialised-K* path),
+// zero padded.  Element (panel, ep, pair, which, lane) holds W[16E + (l&15)][4s + (l>>4)] and
+// the same at s+1 (E = 2ep + which, s = panel*ns_panel + 2*pair).
+__device__ void pack_range(long long t0, long long stride, d2* __restrict__ out,
+                           const double* __restrict__ kinv, long long ld, int n, int n_pad,
+                           int ns_panel, int n_obj) {
   const long long per_obj = (long long)n_pad * n_pad / 2;
   const long long total = per_obj * n_obj;
   const int n_ep = n_pad / 32;
   const int npair = ns_panel / 2;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
+  for (long long t = t0; t < total; t += stride) {
     const int o = (int)(t / per_obj);
     long long r = t - (long long)o * per_obj;
     const int lane = (int)(r & 63); r >>= 6;
@@ -308,27 +247,6 @@ __global__ void pack_kernel(d2* __restrict__ out, const double* __restrict__ kin
     v.y = (row < n && col1 < n) ? wo[(long long)row * ld + col1] : 0.0;
     out[t] = v;
   }
-}
-
-// alpha[o][f] = sum_e Kinv[o][f][e] * (y[e][o] - pm[o])   (numba_kernels.py:477-483),
-// e ascending, zero for padded rows.  One wave per row: lane-strided partial sums then
-// a shuffle tree (order differs from BLAS dgemv only in the last bits).
-__global__ void alpha_kernel(double* __restrict__ alpha, const double* __restrict__ kinv,
-                             long long ld, const double* __restrict__ y, long long ld_y, int n,
-                             int n_pad, int n_obj, FusedArgs a) {
-  const int lane = threadIdx.x & 63;
-  const long long row_id = blockIdx.x * (long long)(blockDim.x / 64) + (threadIdx.x >> 6);
-  if (row_id >= (long long)n_obj * n_pad) return;
-  const int o = (int)(row_id / n_pad), f = (int)(row_id % n_pad);
-  double s = 0.0;
-  if (f < n) {
-    const double* wr = kinv + (long long)o * ld * ld + (long long)f * ld;
-    const double pm = a.pm[o];
-    for (int e = lane; e < n; e += 64) s = __builtin_fma(wr[e], y[(long long)e * ld_y + o] - pm, s);
-  }
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
-  if (lane == 0) alpha[row_id] = s;
 }
 
 // Merge the per-wave lists [n_lists][q] into the final top-q (one workgroup, 16 waves).
@@ -434,12 +352,12 @@ __global__ void selftest_mfma_kernel(const double* a, const double* b, double* d
 
 // float4 entry (o, block, kq, b, lane) = {W[row][col0 + t], t = 0..3}, row = 64 ep + 16 b +
 // (lane & 15), col0 = 64 c + 16 kq + 4 (lane >> 4); W = triu(sym(K^-1)) with halved diagonal.
-__global__ void pack32_kernel(f4* __restrict__ out, const double* __restrict__ kinv, long long ld,
-                              int n, int n_pad, int n_obj) {
+__device__ void pack32_range(long long t0, long long stride, f4* __restrict__ out,
+                             const double* __restrict__ kinv, long long ld, int n, int n_pad,
+                             int n_obj) {
   const int nch = n_pad / 64;
   const long long per_obj = c32_blocks(nch) * 1024;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < per_obj * n_obj;
-       t += (long long)gridDim.x * blockDim.x) {
+  for (long long t = t0; t < per_obj * n_obj; t += stride) {
     const int o = (int)(t / per_obj);
     long long r = t - (long long)o * per_obj;
     const int lane = (int)(r & 63); r >>= 6;
@@ -481,6 +399,92 @@ __global__ void pack32_kernel(f4* __restrict__ out, const double* __restrict__ k
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Per-call preparation, ONE launch (blocks by role):
+//   [0, pack_blocks)               W packed into the kernel's MFMA stream (pack_cm_range /
+//                                  pack_range / pack32_range);
+//   [.., + alpha_blocks)           alpha[o][f] = sum_e K^-1[o][f][e] (y[e][o] - pm[o])
+//                                  (numba_kernels.py:477-483), one wave per row, e ascending
+//                                  per lane then a shuffle tree;
+//   last block                     training rows: xpad (original; padded rows 1e200 so their
+//                                  K* is exactly 0) and xc = x - x_0 (centred); the
+//                                  separable-grid precondition flag (every training point's last
+//                                  coordinate an integer on the grid's last axis); the
+//                                  evaluated points padded to [n_excl][DIM].
+// ---------------------------------------------------------------------------------------
+struct PrepArgs {
+  int pack_mode;                         // 0 chunk-major (cm), 1 panels (kmem), 2 f32 (cm32)
+  void* wpack;
+  const double* kinv;
+  long long ld_k;
+  int upper, n, n_pad, ns, n_obj;
+  int pack_blocks, alpha_blocks;
+  double* alpha;
+  const double* y;
+  long long ld_y;
+  double pm[BO_MAX_OBJ];
+  int rows;                              // training-row preparation (not on the kmem path)
+  double *xpad, *xc;
+  const double* x;
+  int dim, DIM;
+  int* sep_flag;                         // NULL: no separable grid check
+  long long sep_lo;
+  int sep_S;
+  double* excl;
+  const double* excl_in;
+  int n_excl;
+};
+
+__global__ __launch_bounds__(256) void predict_prep_kernel(const PrepArgs p) {
+  const int tid = threadIdx.x;
+  int b = blockIdx.x;
+  if (b < p.pack_blocks) {
+    const long long t0 = (long long)b * 256 + tid, stride = (long long)p.pack_blocks * 256;
+    if (p.pack_mode == 0) pack_cm_range(t0, stride, (d2*)p.wpack, p.kinv, p.ld_k, p.upper, p.n, p.n_pad, p.n_obj);
+    else if (p.pack_mode == 1) pack_range(t0, stride, (d2*)p.wpack, p.kinv, p.ld_k, p.n, p.n_pad, p.ns, p.n_obj);
+    else pack32_range(t0, stride, (f4*)p.wpack, p.kinv, p.ld_k, p.n, p.n_pad, p.n_obj);
+    return;
+  }
+  b -= p.pack_blocks;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (b < p.alpha_blocks) {
+    const long long row_id = (long long)b * 4 + wave;
+    if (row_id >= (long long)p.n_obj * p.n_pad) return;
+    const int o = (int)(row_id / p.n_pad), f = (int)(row_id % p.n_pad);
+    double s = 0.0;
+    if (f < p.n) {
+      const double* wr = p.kinv + (long long)o * p.ld_k * p.ld_k + (long long)f * p.ld_k;
+      const double pm = p.pm[o];
+      for (int e = lane; e < p.n; e += 64) s = __builtin_fma(wr[e], p.y[(long long)e * p.ld_y + o] - pm, s);
+    }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+    if (lane == 0) p.alpha[row_id] = s;
+    return;
+  }
+  if (!p.rows) return;
+  int sep_bad = 0;
+  for (int f = tid; f < p.n_pad; f += 256) {
+    for (int k = 0; k < p.DIM; ++k) {
+      const bool real = f < p.n && k < p.dim;
+      const double v = f < p.n ? (real ? p.x[(long long)f * p.dim + k] : 0.0) : 1e200;
+      p.xpad[(long long)f * p.DIM + k] = v;
+      p.xc[(long long)f * p.DIM + k] = f < p.n ? v - (k < p.dim ? p.x[k] : 0.0) : 1e200;
+    }
+    if (f < p.n && p.sep_flag) {
+      const double v = p.x[(long long)f * p.dim + p.dim - 1];
+      const bool ok = v == __builtin_rint(v) && v >= (double)p.sep_lo && v <= (double)(p.sep_lo + p.sep_S - 1);
+      sep_bad |= !ok;
+    }
+  }
+  const int any_bad = __syncthreads_or(sep_bad);
+  if (tid == 0 && p.sep_flag) *p.sep_flag = any_bad ? 1 : 0;
+  for (int t = tid; t < p.n_excl * p.DIM; t += 256) {
+    const int r = t / p.DIM, k = t - r * p.DIM;
+    p.excl[t] = k < p.dim ? p.excl_in[(long long)r * p.dim + k] : 0.0;
+  }
+}
 
 __global__ void selftest_mfma32_kernel(const float* a, const float* b, float* d) {
   const int l = threadIdx.x;
@@ -546,10 +550,8 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
     pl->cm = true;
     pl->n_pad = n_pad;
     pl->ns = n_pad / 4;
-    pl->dotx = d->cand_kind != BO_CAND_GRID && !(d->mode & BO_PREDICT_DENSE);
-    // non-SEP layout: rows + alpha, [|x_f|^2 (dot form)], exp table
-    const size_t sq_sz = pl->dotx ? (size_t)n_pad : 0;
-    const size_t plain = base + sq_sz + bo::kExpTab;
+    // non-SEP layout: rows + alpha, exp table
+    const size_t plain = base + bo::kExpTab;
     size_t lds = plain;
     if (d->cand_kind == BO_CAND_GRID && !(d->mode & BO_PREDICT_NO_SEPARABLE)) {
       const long long S = d->grid_shape[d->dim - 1];
@@ -566,13 +568,11 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
         if (lds < plain) lds = plain;          // the non-SEP fallback shares the kernel's LDS
       }
     }
-    pl->off_sqlds = (int)base;
-    pl->off_exp = (int)(base + sq_sz);
+    pl->off_exp = (int)base;
     if (lds > kLdsDoubles) {
       // rows / |x_f|^2 / alpha from global memory; the exp table alone in LDS
       pl->sep = false;
       pl->grows = true;
-      pl->off_sqlds = 0;
       pl->off_exp = 0;
       lds = bo::kExpTab;
     }
@@ -606,13 +606,12 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   pl->off_alpha = align256(w_bytes);
   pl->off_xpad = pl->off_alpha + align256((size_t)d->n_obj * n_pad * sizeof(double));
   pl->off_xc = pl->off_xpad + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
-  pl->off_sq = pl->off_xc + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
-  pl->off_excl = pl->off_sq + align256((size_t)n_pad * sizeof(double));
+  pl->off_excl = pl->off_xc + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
   pl->off_partial = pl->off_excl + align256((size_t)(pl->n_excl + 1) * pl->dim_pad * sizeof(double));
   // partial lists sized for the largest persistent grid any device could use
   pl->off_status = pl->off_partial +
                    align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry));
-  pl->total = pl->off_status + 256 + 256;   // +0: extents (2 x u64), +16: separable-K* flag
+  pl->total = pl->off_status + 256 + 256;   // +16: separable-K* flag
   return BO_OK;
 }
 
@@ -680,10 +679,8 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   double* alpha = (double*)(ws + pl.off_alpha);
   double* xpad = (double*)(ws + pl.off_xpad);
   double* xc = (double*)(ws + pl.off_xc);
-  double* sq = (double*)(ws + pl.off_sq);
   double* excl = (double*)(ws + pl.off_excl);
   TopEntry* partial = (TopEntry*)(ws + pl.off_partial);
-  unsigned long long* ext = (unsigned long long*)(ws + pl.off_status);
   int* sep_flag = (int*)(ws + pl.off_status + 16);
 
   FusedArgs fa;
@@ -722,11 +719,15 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   }
   fa.xpad = xpad;
   fa.xc = xc;
-  fa.sqg = sq;
-  fa.ext = ext;
   fa.excl = d->excl_points ? excl : nullptr;
   fa.wpack = wpack;
+  fa.upper = (pl.cm && !(d->mode & BO_PREDICT_DENSE)) ? 1 : 0;
   fa.wpack_bytes = (unsigned int)((size_t)d->n_obj * pl.n_pad * pl.n_pad * sizeof(double));
+  if (pl.cm) {
+    // contiguous objective streams of 2-KiB pairs (pack_cm_range); the ring wraps at the end
+    fa.w_pairs = (int)(cm_blocks(pl.n_pad / 32, fa.upper) * 4 * d->n_obj);
+    fa.wpack_bytes = (unsigned int)((size_t)fa.w_pairs * 2048);
+  }
   fa.alpha = alpha;
   for (int o = 0; o < d->n_obj; ++o) {
     fa.pm[o] = d->prior_mean[o];
@@ -746,57 +747,49 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.kstar = kstar;
   fa.ks_rows = ks_rows;
 
-  fa.upper = (pl.cm && !(d->mode & BO_PREDICT_DENSE)) ? 1 : 0;
   fa.sep_flag = pl.sep ? sep_flag : nullptr;
   fa.sep_S = pl.sep ? (int)d->grid_shape[d->dim - 1] : 1;
   fa.sep_lo = pl.sep ? d->grid_lo[d->dim - 1] : 0;
   fa.off_tbl = pl.off_tbl;
   fa.off_rw = pl.off_rw;
   fa.rw_cache = pl.rw_cache ? 1 : 0;
-  fa.dotx = pl.dotx ? 1 : 0;
-  fa.off_sq = pl.off_sqlds;
   fa.off_exp = pl.off_exp;
-  BO_CHECK_HIP(hipMemsetAsync(ext, 0, 256 + 32, s));          // extents and the separable flag
-  if (pl.sep) {
-    hipLaunchKernelGGL(sep_check_kernel, dim3((unsigned)((d->n_train + 255) / 256)), dim3(256), 0, s,
-                       d->x_train, (int)d->n_train, d->dim, (long long)fa.sep_lo, fa.sep_S, sep_flag);
-    BO_CHECK_HIP(hipGetLastError());
-  }
   {
-    const long long total = (long long)d->n_obj * pl.n_pad * pl.n_pad / 2;
-    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    if (pl.fp32)
-      hipLaunchKernelGGL(pack32_kernel, dim3(blocks), dim3(256), 0, s, (f4*)wpack, d->kinv, d->ld_k,
-                         (int)d->n_train, pl.n_pad, d->n_obj);
-    else if (pl.cm)
-      hipLaunchKernelGGL(pack_cm_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k, fa.upper,
-                         (int)d->n_train, pl.n_pad, d->n_obj);
-    else
-      hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, wpack, d->kinv, d->ld_k,
-                         (int)d->n_train, pl.n_pad, pl.ns, d->n_obj);
+    PrepArgs pa;
+    memset(&pa, 0, sizeof(pa));
+    pa.pack_mode = pl.fp32 ? 2 : (pl.cm ? 0 : 1);
+    pa.wpack = wpack;
+    pa.kinv = d->kinv;
+    pa.ld_k = d->ld_k;
+    pa.upper = fa.upper;
+    pa.n = (int)d->n_train;
+    pa.n_pad = pl.n_pad;
+    pa.ns = pl.ns;
+    pa.n_obj = d->n_obj;
+    const long long total = pl.fp32 ? c32_blocks(pl.n_pad / 64) * 1024 * d->n_obj
+                          : pl.cm ? cm_blocks(pl.n_pad / 32, fa.upper) * 512 * d->n_obj
+                                  : (long long)d->n_obj * pl.n_pad * pl.n_pad / 2;
+    pa.pack_blocks = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+    pa.alpha_blocks = (int)(((long long)d->n_obj * pl.n_pad + 3) / 4);
+    pa.alpha = alpha;
+    pa.y = d->y_train;
+    pa.ld_y = d->ld_y;
+    for (int o = 0; o < d->n_obj; ++o) pa.pm[o] = d->prior_mean[o];
+    pa.rows = kmem ? 0 : 1;
+    pa.xpad = xpad;
+    pa.xc = xc;
+    pa.x = d->x_train;
+    pa.dim = d->dim;
+    pa.DIM = pl.dim_pad;
+    pa.sep_flag = pl.sep ? sep_flag : nullptr;
+    pa.sep_lo = fa.sep_lo;
+    pa.sep_S = fa.sep_S;
+    pa.excl = excl;
+    pa.excl_in = d->excl_points;
+    pa.n_excl = (kmem || !d->excl_points) ? 0 : pl.n_excl;
+    hipLaunchKernelGGL(predict_prep_kernel, dim3((unsigned)(pa.pack_blocks + pa.alpha_blocks + 1)), dim3(256),
+                       0, s, pa);
     BO_CHECK_HIP(hipGetLastError());
-    const long long rows = (long long)d->n_obj * pl.n_pad;
-    hipLaunchKernelGGL(alpha_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, alpha,
-                       d->kinv, d->ld_k, d->y_train, d->ld_y, (int)d->n_train, pl.n_pad,
-                       d->n_obj, fa);
-    BO_CHECK_HIP(hipGetLastError());
-    if (!kmem) {
-      hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((pl.n_pad + 255) / 256)), dim3(256), 0, s,
-                         xpad, xc, sq, ext, d->x_train, (int)d->n_train, pl.n_pad, d->dim, pl.dim_pad);
-      BO_CHECK_HIP(hipGetLastError());
-      if (pl.cm && fa.upper && pl.dotx && d->n_cand > 0) {
-        const long long nb = (d->n_cand + 255) / 256;
-        hipLaunchKernelGGL(cand_extent_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(256), 0, s,
-                           ext, fa);
-        BO_CHECK_HIP(hipGetLastError());
-      }
-    }
-    const int cnt = (kmem || !d->excl_points) ? 0 : pl.n_excl * pl.dim_pad;
-    if (cnt > 0) {
-      hipLaunchKernelGGL(pad_points_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, excl,
-                         d->excl_points, pl.n_excl, pl.n_excl, d->dim, pl.dim_pad, 0.0);
-      BO_CHECK_HIP(hipGetLastError());
-    }
   }
   if (d->n_cand == 0) {
     if (d->topq > 0) {

@@ -27,10 +27,6 @@ constexpr int kPF = 4;                  // W prefetch ring depth (pairs of k-ste
 constexpr int kCMaxEp = 16;             // E-pairs (32 rows each) whose accumulators one wave holds
 constexpr int kC32MaxEp = 16;           // E-quads (64 rows each) per group of the f32 kernel
 constexpr int kExpTab = 256;            // 2^(j/256) table of exp2_tab
-// the dot-form exponent is used only while max|nl2| (max_f |x_f - z|^2 + max_c |c - z|^2) stays
-// below this bound: its cancellation error is ~4 eps times that, i.e. <= 1e-8 absolute in the
-// exponent (K* relative error 1e-8 against the 1e-5 pv variance tolerance)
-constexpr double kDotxLimit = 1.0e7;
 
 struct FusedArgs {
   int n_obj, dim, n_train, n_pad;       // n_pad = padded training rows (multiple of 32 / 64)
@@ -42,11 +38,10 @@ struct FusedArgs {
   const void* cand;
   const double* xpad;                    // [n_pad][DIM] training rows, padded rows = 1e200 (global)
   const double* xc;                      // [n_pad][DIM] rows minus row 0 (the centre z) (global)
-  const double* sqg;                     // [n_pad] |xc_f|^2, inf for padded rows (global)
-  const unsigned long long* ext;         // [2] max |xc_f|^2 (f < N), max |c - z|^2 (bit patterns)
   const double* excl;                    // [n_excl][DIM] evaluated points (global), NULL = x_train
-  const d2* wpack;                       // packed W (pack_cm_kernel / pack_kernel / pack32 layout)
+  const d2* wpack;                       // packed W (pack_cm_range / pack_range / pack32_range layout)
   unsigned int wpack_bytes;
+  int w_pairs;                           // cm: 2-KiB pairs of all objectives' contiguous streams
   const double* alpha;                   // [n_obj][n_pad] = K^-1 (y - pm) (global)
   double pm[BO_MAX_OBJ], pv[BO_MAX_OBJ], nhl[BO_MAX_OBJ], beta[BO_MAX_OBJ], rsq_pv[BO_MAX_OBJ];
   double *mu, *var, *std_mu, *std_var, *ucb, *acq;
@@ -61,8 +56,6 @@ struct FusedArgs {
   long long sep_lo;
   int off_tbl, off_rw;
   int rw_cache;                          // SEP row factors kept for every objective (LDS permitting)
-  int dotx;                              // explicit candidates, upper form: dot-form exponent allowed
-  int off_sq;                            // LDS offset (doubles) of |xc_f|^2 (LDS-resident rows)
   int off_exp;                           // LDS offset (doubles) of the 2^(j/256) table
   SobolArgs sob;                         // kind BO_CAND_SOBOL: direction numbers, lo, scale
 };
@@ -71,15 +64,14 @@ struct FusedArgs {
 struct Plan {
   int n_pad, ns, n_panels, dim_pad, n_excl;
   bool multi;
-  size_t off_alpha, off_xpad, off_xc, off_sq, off_excl, off_partial, off_status, total;
+  size_t off_alpha, off_xpad, off_xc, off_excl, off_partial, off_status, total;
   bool cm;               // chunk-major kernel (cm_predict_kernel)
   bool sep;              // ... with the integer-grid K* generation
   bool grows;            // ... training rows / alpha read from global memory (N beyond LDS)
-  bool dotx;             // ... explicit candidates: dot-form exponent (subject to the device gate)
   int off_tbl, off_rw;   // LDS offsets in doubles
   bool rw_cache;         // SEP row factors cached per objective
   bool fp32;             // cm32_predict_kernel (BO_PREDICT_FP32)
-  int off_sqlds, off_exp;
+  int off_exp;
   int grid, waves;       // persistent grid, waves per workgroup
   long long n_tiles;
   size_t lds;
@@ -218,30 +210,6 @@ __device__ __forceinline__ double exp2_tab(double t, const double* tb) {
   return __builtin_ldexp(p * tb[ki & (kExpTab - 1)], ki >> 8);
 }
 
-#ifdef BO_ABL_OLDEXP
-// diagnostic build only: the round-1 table-free 2^t (range reduction to [-1/2, 1/2], degree 13)
-__device__ __forceinline__ double exp2_old(double t) {
-  const double x = fmax(t, -1100.0);
-  const double n = __builtin_rint(x);
-  const double r = x - n;
-  double p = 1.36914888539041241e-12;
-  p = __builtin_fma(p, r, 2.56784359934881958e-11);
-  p = __builtin_fma(p, r, 4.44553827187081007e-10);
-  p = __builtin_fma(p, r, 7.05491162080112088e-09);
-  p = __builtin_fma(p, r, 1.01780860092396960e-07);
-  p = __builtin_fma(p, r, 1.32154867901443053e-06);
-  p = __builtin_fma(p, r, 1.52527338040598377e-05);
-  p = __builtin_fma(p, r, 1.54035303933816061e-04);
-  p = __builtin_fma(p, r, 1.33335581464284411e-03);
-  p = __builtin_fma(p, r, 9.61812910762847688e-03);
-  p = __builtin_fma(p, r, 5.55041086648215762e-02);
-  p = __builtin_fma(p, r, 2.40226506959100694e-01);
-  p = __builtin_fma(p, r, 6.93147180559945286e-01);
-  p = __builtin_fma(p, r, 1.0);
-  return __builtin_ldexp(p, (int)n);
-}
-#define exp2_tab(t, tb) exp2_old(t)
-#endif
 
 // Nested guards over the unrolled E-pair bodies: body E runs iff E < n, and is entered only
 // from body E - 1 (see chunk_step in cm_tiles).
@@ -265,14 +233,13 @@ struct EpChain<N, N> {
 //   SEP (integer 'ij' grid): rv[f] * T[rb[f] - jl] (row factor times the last-axis table);
 //   otherwise the exponent in base 2 with pv folded in, t = nl2 |x_f - c|^2 + log2 pv
 //   (nl2 = nhl log2 e), then exp2_tab.  Coordinates are CENTRED on z = training row 0 (xs holds
-//   x_f - z, c is c - z): distances are translation invariant and the centring keeps the dot
-//   form below exact enough for coordinates far from the origin.
-//   DOTX: t = nl2 |x_f|^2 + (nl2 |c|^2 + log2 pv) + sum_k x_fk (-2 nl2 c_k), |x_f|^2 from sq[]:
-//   DIM + 1 FMAs instead of 2 DIM + 1; used only under the kDotxLimit gate.
-template <int DIM, bool SEP, bool DOTX = false>
+//   x_f - z, c is c - z): distances are translation invariant, and f64 differences of centred
+//   coordinates keep full precision for point sets far from the origin.  (Round 1's dot form
+//   nl2 (|x|^2 + |c|^2 - 2 x.c) saved DIM operations per value but cancels catastrophically
+//   when |x| >> ls; with the table exp2 the direct form measures as fast, so it is gone.)
+template <int DIM, bool SEP>
 struct KRows {
-  const double* sq;   // DOTX: [n_pad] |x_f|^2 (inf for padded rows)
-  double cj, nl2, lpv, dk[DIM];
+  double nl2, lpv;
   const double* rv;   // SEP: [n_pad] pv * R(f) (0 for padded rows)
   const int* rb;      // SEP: [n_pad] table index base (x_f,last - lo_last) + S - 1; jl = col0 + lane
   const double* tb;   // SEP: objective's table T; otherwise the 2^(j/256) table
@@ -281,17 +248,6 @@ struct KRows {
   int jl;
   __device__ __forceinline__ double at(int f) const {
     if (SEP) return rv[f] * tb[rb[f] - jl];
-    if (DOTX) {
-      const d2* r = (const d2*)(xs + f * DIM);
-      double t = __builtin_fma(nl2, sq[f], cj);
-#pragma unroll
-      for (int k = 0; k < DIM / 2; ++k) {
-        const d2 x = r[k];
-        t = __builtin_fma(x.x, dk[2 * k], t);
-        t = __builtin_fma(x.y, dk[2 * k + 1], t);
-      }
-      return exp2_tab(t, tb);
-    }
     return exp2_tab(__builtin_fma(sqdist<DIM>(xs, f, c), nl2, lpv), tb);
   }
   // the 8 values of 32-row chunk `ch` this lane feeds to the MFMAs: rows 32 ch + 4 s + g
@@ -307,9 +263,9 @@ struct KRows {
 // of the mean) completes under MFMAs instead of stalling the wave before the chunk:
 //   s0: rv[f], rb[f], alpha[f] loads     s1: table loads T[rb - jl]     s2: the products.
 // The exp path (!SEP) is VALU work that serialises with f64 MFMAs anyway: all of it in s2.
-template <int DIM, bool SEP, bool DOTX = false>
+template <int DIM, bool SEP>
 struct KGen {
-  using KR = KRows<DIM, SEP, DOTX>;
+  using KR = KRows<DIM, SEP>;
   double rv[8], tv[8];
   int rb[8];
   __device__ __forceinline__ void s0(const KR& K, const double* al, bool mu_on, int ch,
@@ -373,13 +329,12 @@ struct KGen {
 // GROWS: the training rows, |x_f|^2 and alpha are read from global memory (L2-resident)
 // instead of LDS, for N whose rows do not fit the 160 KiB LDS (the reference has no N cap).
 // ---------------------------------------------------------------------------------------
-template <int DIM, bool SEP, bool UPPER, bool DOTX, bool GROWS>
+template <int DIM, bool SEP, bool UPPER, bool GROWS>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   constexpr bool upper = UPPER;
   // training rows (SEP: original grid coordinates; otherwise centred on z = row 0), alpha
   const double* xs = GROWS ? a.xc : smem;
   const double* alpha = GROWS ? a.alpha : smem + (size_t)a.n_pad * DIM;
-  const double* sqv = GROWS ? a.sqg : smem + a.off_sq;
   const double* etab = smem + a.off_exp;                    // 2^(j/256) (!SEP)
   const double* tbl = smem + a.off_tbl;                     // [n_obj][2S - 1] (SEP)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -396,10 +351,15 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   const int TS = 2 * a.sep_S - 1;
   const int nch = a.n_pad / 32;
   const int last = a.dim - 1;
-  const int w_obj = a.n_pad * a.n_pad * 8;
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
   const int voff = lane * 16;
+  // The W ring streams the objectives' packed streams back to back and wraps at the end, so it
+  // runs on across objectives and tiles: primed once per kernel, never drained in between.
+  // fpos = the next pair to fetch (modulo w_pairs, wave-uniform scalar arithmetic).
+  d2 wa[kPF], wb[kPF];
+  prime_ring(wr, voff, 0, wa, wb);
+  int fpos = kPF % a.w_pairs;
   // the centre z (training row 0) of the non-SEP generation
   double z[DIM];
 #pragma unroll
@@ -464,7 +424,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
     double acq = 0.0;
     for (int o = 0; o < a.n_obj; ++o) {
       if (SEP && !a.rw_cache) row_pass(c, o, o + 1);
-      KRows<DIM, SEP, DOTX> K;
+      KRows<DIM, SEP> K;
       K.rv = rv + (a.rw_cache ? (size_t)o * a.n_pad : 0); K.rb = rb;
       K.tb = SEP ? tbl + (size_t)o * TS : etab;
       K.xs = xs;
@@ -473,18 +433,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       K.jl = SEP ? col0 + jl : jl;   // T index = rb[f] - (col0 + jl) = x_f,last - c_last + S - 1
 #pragma unroll
       for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
-      if (DOTX) {
-        K.sq = sqv;
-        double cc = 0.0;
-#pragma unroll
-        for (int k = 0; k < DIM; ++k) { cc = __builtin_fma(c[k], c[k], cc); K.dk[k] = -2.0 * K.nl2 * c[k]; }
-        K.cj = __builtin_fma(K.nl2, cc, K.lpv);
-      }
       const double* al = alpha + (size_t)o * a.n_pad;
-      const int base = o * w_obj;
-      d2 wa[kPF], wb[kPF];
-      prime_ring(wr, voff, base, wa, wb);
-      int pos = 0;
       double mpart = 0.0, qpart = 0.0;
       d4 acc[kCMaxEp][2];
       // E-pairs in groups of kCMaxEp (the accumulators one wave holds: 512 rows); a group
@@ -502,7 +451,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         // sets alternate: no register copies between the chunks).  Branch-free: the last chunk
         // regenerates itself (chn clamped) and groups after the first add 0 x alpha to mu.
         const bool mu_on = e0 == 0;
-        KGen<DIM, SEP, DOTX> gen;
+        KGen<DIM, SEP> gen;
         auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8], const double (&A)[8],
                               double (&An)[8]) {
           // next chunk: ascending (dense) / descending (upper); the last one regenerates itself
@@ -526,10 +475,10 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
               acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
               acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
-              const int so = base + ((pos + kPF) << 11);
+              const int so = fpos << 11;
               wa[pp] = wload(wr, voff, so);
               wb[pp] = wload(wr, voff, so + 1024);
-              ++pos;
+              fpos = fpos + 1 == a.w_pairs ? 0 : fpos + 1;
               if constexpr (e == 0) {
                 if (pp == 0) {
                   __builtin_amdgcn_sched_barrier(0);
@@ -586,7 +535,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         // E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence and multiplied after
         // its FMAs, so the fences' wait states cover the LDS round trips.
         if (!upper) {
-          KGen<DIM, SEP, DOTX> gq[2];
+          KGen<DIM, SEP> gq[2];
           double S[2][8];
           gq[0].s0k(K, e0, g);
           gq[0].s1(K);
@@ -708,34 +657,12 @@ __global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
     }
   } else {
     for (int t = tid; t < kExpTab; t += blockDim.x) smem[a.off_exp + t] = exp2((double)t / kExpTab);
-    if (!GROWS && a.dotx)
-      for (int f = tid; f < a.n_pad; f += blockDim.x) smem[a.off_sq + f] = a.sqg[f];
-  }
-  // dot-form gate (explicit candidates): max|nl2| (max_f |x_f - z|^2 + max_c |c - z|^2) over
-  // the training rows and the call's candidates (prep kernels, bit patterns of non-negative
-  // doubles max-reduced as integers; NaN compares false) must stay below kDotxLimit
-  bool dotx = false;
-  if (!GRID && UPPER && a.dotx) {
-    const double rx = __longlong_as_double((long long)a.ext[0]);
-    const double rc = __longlong_as_double((long long)a.ext[1]);
-    double nl = 0.0;
-    for (int o = 0; o < a.n_obj; ++o) nl = fmax(nl, fabs(a.nhl[o] * 1.4426950408889634));
-    dotx = nl * (rx + rc) <= bo::kDotxLimit;
-#ifdef BO_ABL_FORCEDOTX
-    dotx = true;
-#endif
-#ifdef BO_ABL_NODOTX
-    dotx = false;
-#endif
   }
   __syncthreads();
   if constexpr (GRID && !GROWS) {
-    if (sep) { cm_tiles<DIM, true, UPPER, false, false>(a, smem); return; }
+    if (sep) { cm_tiles<DIM, true, UPPER, false>(a, smem); return; }
   }
-  if constexpr (!GRID && UPPER) {
-    if (dotx) { cm_tiles<DIM, false, UPPER, true, GROWS>(a, smem); return; }
-  }
-  cm_tiles<DIM, false, UPPER, false, GROWS>(a, smem);
+  cm_tiles<DIM, false, UPPER, GROWS>(a, smem);
 }
 
 template <int DIM, bool GRID, bool UPPER, bool GROWS>

@@ -1,6 +1,6 @@
-"""Summarise the rocprofv3 PMC passes of scripts/pmc.sh for the fused C3 kernel.
+"""Summarise the rocprofv3 PMC passes of scripts/pmc.sh / pmc_cfg.sh for the fused kernel.
 
-    python scripts/pmc_summary.py gpurun_out/pmc profiles/r01_c3_pmc.json
+    python scripts/pmc_summary.py gpurun_out/pmc profiles/r01_c3_pmc.json [WORKLOAD ALG_BYTES KERNEL]
 
 Per-launch means over the cm_predict_kernel dispatches of each pass.  HBM bytes follow the
 MI355X guide's HBM/rocprofv3 section: FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
@@ -17,7 +17,7 @@ from collections import defaultdict
 KERNEL = "cm_predict_kernel"
 
 
-def main(src, dst):
+def main(src, dst, workload="C3", alg_bytes=40 * 1048576, kernel_label="cm_predict_kernel<2, true, true>"):
     vals = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(src, "p*", "*counter_collection.csv"))):
         with open(f) as fh:
@@ -31,22 +31,26 @@ def main(src, dst):
                 for k, v in d.items():
                     vals[k].append(v)
     mean = {k: sum(v) / len(v) for k, v in vals.items()}
-    out = {"workload": "C3", "kernel": "cm_predict_kernel<2, true, true>",
+    out = {"workload": workload, "kernel": kernel_label,
            "counters_per_launch": mean, "launches_per_counter": {k: len(v) for k, v in vals.items()}}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         fetch = 2.0 * mean["FETCH_SIZE"] * 1024.0       # gfx950 16-B-read correction
         write = mean["WRITE_SIZE"] * 1024.0
         out.update({"fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
                     "hbm_bytes_per_launch": fetch + write,
-                    "algorithmic_bytes_per_launch": 40 * 1048576,
+                    "algorithmic_bytes_per_launch": alg_bytes,
+                    "traffic_ratio": (fetch + write) / alg_bytes,
                     "note": "FETCH_SIZE x2 (gfx950 16-B streaming-read correction), KiB -> B; "
-                            "algorithmic = 40 B/candidate (mu, var, acq f64 written; grid generated)"})
+                            "algorithmic = outputs written (+ explicit coordinates read)"})
     if "SQ_INSTS_MFMA" in mean and "SQ_INSTS_VALU" in mean:
         out["valu_per_mfma"] = mean["SQ_INSTS_VALU"] / max(mean["SQ_INSTS_MFMA"], 1.0)
+    if "SQ_WAIT_INST_ANY" in mean and "SQ_BUSY_CYCLES" in mean:
+        out["wait_inst_any_per_busy_cycle"] = mean["SQ_WAIT_INST_ANY"] / max(mean["SQ_BUSY_CYCLES"], 1.0)
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    a = sys.argv[1:]
+    main(a[0], a[1], *([a[2], float(a[3])] + a[4:5] if len(a) > 2 else []))
