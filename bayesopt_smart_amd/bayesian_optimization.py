@@ -172,6 +172,8 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
             })
             for cb in callbacks:
                 cb(state)
+    if isinstance(kernel_matrices, np.ndarray):   # the reference mutates it in place (update_k)
+        kernel_matrices[...] = bufs.kernel_matrices.cpu().numpy().reshape(kernel_matrices.shape)
     for name, a in (("mu", mu_objectives), ("var", variance_objectives), ("smu", std_mu_objectives),
                     ("svar", std_variance_objectives), ("ucb", ucb), ("acq", acquisition_values)):
         if isinstance(a, np.ndarray):   # numpy callers get their arrays filled, as in the reference
@@ -180,6 +182,25 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
                    "ucb": bufs.ucb, "acq": bufs.acquisition_values}[name]
             a[...] = src.cpu().numpy()
     return x_vector, y_vector, last_eval + 1
+
+
+def _check_limits(n_obj, dim, total_samples, batch_size):
+    """Fail in the constructor -- before any objective evaluation -- on shapes the device path
+    cannot run (the reference would hit them only mid-loop, if at all)."""
+    if not 1 <= n_obj <= _lib.MAX_OBJ:
+        raise ValueError(f"n_objectives must be in [1, {_lib.MAX_OBJ}] (got {n_obj})")
+    if not 1 <= dim <= _lib.MAX_DIM:
+        raise ValueError(f"the input dimension must be in [1, {_lib.MAX_DIM}] (got {dim})")
+    if batch_size < 1:
+        raise ValueError("batch_size must be >= 1")
+    d = _lib.PredictDesc()
+    d.n_obj, d.dim, d.n_train, d.n_cand, d.cand_kind, d.topq = n_obj, dim, total_samples, 1, _lib.CAND_GRID, 0
+    for k in range(dim):
+        d.grid_shape[k] = 1
+    lib = _lib.load()
+    if lib.bo_predict_workspace_size(d) == 0 or lib.bo_invert_k_workspace_size(n_obj, total_samples) == 0:
+        raise ValueError(f"total_samples = {total_samples} exceeds the device path's limits "
+                         f"(predict: N <= 16384 and n_obj N^2 doubles < 2 GiB)")
 
 
 class BayesianOptimization:
@@ -216,6 +237,7 @@ class BayesianOptimization:
                            else CandidateSet.explicit(explicit, self.device))
         self._input_space = None
         self.total_samples = self.initial_samples + self.n_iterations * self.batch_size
+        _check_limits(n_objectives, self.dim, self.total_samples, self.batch_size)
         self.x_vector = np.zeros((self.total_samples, self.dim), dtype=NUMBA_FLOAT_TYPE)
         self.y_vector = np.zeros((self.total_samples, n_objectives), dtype=NUMBA_FLOAT_TYPE)
         self._buffers = DeviceBuffers(n_objectives, self.total_samples, self.candidates.n, self.device)

@@ -354,12 +354,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
   const int voff = lane * 16;
-  // The W ring streams the objectives' packed streams back to back and wraps at the end, so it
-  // runs on across objectives and tiles: primed once per kernel, never drained in between.
-  // fpos = the next pair to fetch (modulo w_pairs, wave-uniform scalar arithmetic).
-  d2 wa[kPF], wb[kPF];
-  prime_ring(wr, voff, 0, wa, wb);
-  int fpos = kPF % a.w_pairs;
+  const int w_obj = a.w_pairs / a.n_obj * 2048;             // bytes of one objective's stream
   // the centre z (training row 0) of the non-SEP generation
   double z[DIM];
 #pragma unroll
@@ -434,6 +429,13 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #pragma unroll
       for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
       const double* al = alpha + (size_t)o * a.n_pad;
+      // W ring: primed per objective (a ring running on across objectives and tiles measured
+      // 7 % slower at C4 -- its modular refill offsets defeat the immediate-offset addressing --
+      // and no faster at C2)
+      const int base = o * w_obj;
+      d2 wa[kPF], wb[kPF];
+      prime_ring(wr, voff, base, wa, wb);
+      int pos = 0;
       double mpart = 0.0, qpart = 0.0;
       d4 acc[kCMaxEp][2];
       // E-pairs in groups of kCMaxEp (the accumulators one wave holds: 512 rows); a group
@@ -441,11 +443,14 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       // regenerates their K*.  One group when N <= 512.
       for (int e0 = 0; e0 < nch; e0 += kCMaxEp) {
         const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
-#pragma unroll
-        for (int e = 0; e < kCMaxEp; ++e) {
+        // zero the group's eN accumulator pairs only (small N: 4 of 16 at C2, each pair is 16
+        // AGPR writes)
+        auto zero_acc = [&](auto e_c) {
+          constexpr int e = decltype(e_c)::value;
           acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
           acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
-        }
+        };
+        EpChain<0, kCMaxEp>::run(zero_acc, eN);
         // one chunk: MFMAs from register set B while the next chunk's K* (and its alpha
         // values, An) is generated into Bn in three stages inside E-pair 0's MFMA stream (the
         // sets alternate: no register copies between the chunks).  Branch-free: the last chunk
@@ -475,10 +480,10 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
               acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
               acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
-              const int so = fpos << 11;
+              const int so = base + ((pos + kPF) << 11);
               wa[pp] = wload(wr, voff, so);
               wb[pp] = wload(wr, voff, so + 1024);
-              fpos = fpos + 1 == a.w_pairs ? 0 : fpos + 1;
+              ++pos;
               if constexpr (e == 0) {
                 if (pp == 0) {
                   __builtin_amdgcn_sched_barrier(0);

@@ -44,13 +44,18 @@ def as_dev(x, device, dtype=F64):
 
 
 class Workspace:
-    """Grow-only device scratch buffer (one per device)."""
+    """Grow-only device scratch buffer, one per (device, stream): calls in flight on different
+    streams never share scratch (their packed W, alpha and partial top-q lists would collide).
+    A call on a stream reuses the buffer only after its previous calls on that same stream
+    (stream order), so no extra synchronisation is needed.  A grown buffer's old storage is
+    released through the caching allocator, which is stream-ordered as well."""
 
     _cache = {}
 
     @classmethod
-    def get(cls, nbytes, device):
-        key = (device.type, device.index)
+    def get(cls, nbytes, device, stream=None):
+        st = stream_handle(device) if stream is None else stream
+        key = (device.type, device.index, int(st or 0))
         buf = cls._cache.get(key)
         if buf is None or buf.numel() < nbytes:
             buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

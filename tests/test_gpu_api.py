@@ -243,3 +243,42 @@ def test_orchestrator_exact_hvi_acquisition(bo):
     assert np.all(np.abs(acq[sub] - brute) <= 1e-7 * np.maximum(1.0, np.abs(brute)))
     grid = O.grid_points([(0, 300), (0, 300)])
     np.testing.assert_array_equal(seen[0], O.select_next_batch(grid, ref, x, 3))
+
+
+@pytest.mark.parametrize("it", [6, 9, 12])
+def test_demo_trajectory_replay_each_iteration(bo, it):
+    """Every recorded iteration of the reference's headless demo run (G6), replayed on the
+    device from the reference's own state at that iteration -- evaluated points x[:it], y[:it],
+    the Powell-fitted length scales and prior variances it used (numba_kernels.py:318-321
+    updates them in place), the initial prior mean: the acquisition values of the reference's
+    top-64 candidates within 1e-5 max(1, |v|), and the selected batch equal to the reference's
+    (tie-aware: the reference's argsort order is unspecified within 10x the tolerance)."""
+    import torch
+    d = load_golden("g6_trajectory")
+    x, y = d["x_final"][:it], d["y_final"][:it]
+    hyp = d[f"hyper_{it}"]
+    ls, pv, pm = hyp[:2].copy(), hyp[2:].copy(), d["pm0"]
+    km = np.zeros((2, it, it))
+    bo.kernels.update_k(km, x, 0, it, pv, ls)
+    kinv = bo.kernels.invert_k(it, km)
+    cands = bo.CandidateSet.grid([(0, 300), (0, 300)])
+    r = bo.predict_acquire(x, y, kinv, cands, pm, pv, ls, np.array([2.0, 2.0]), outputs=("acq",), topq=3)
+    torch.cuda.synchronize()
+    acq = r["acq"].cpu().numpy()
+    top_idx, top_val = d[f"acq_top_idx_{it}"], d[f"acq_top_val_{it}"]
+    tol = 1e-5 * np.maximum(1.0, np.abs(top_val))
+    assert np.all(np.abs(acq[top_idx] - top_val) <= tol)
+    # the reference's order over non-evaluated candidates (select_next_batch, acquisition.py:134-142)
+    grid = O.grid_points([(0, 300), (0, 300)])
+    ev = {tuple(p) for p in x.astype(np.int64)}
+    keep = [t for t in range(top_idx.size) if tuple(grid[top_idx[t]]) not in ev]
+    ridx, rval = top_idx[keep], top_val[keep]
+    sel = r["top_idx"].cpu().numpy()
+    np.testing.assert_array_equal(grid[ridx[:3]], d[f"x_next_{it}"])     # the fixture's own batch
+    for t in range(3):
+        tt = 1e-5 * max(1.0, abs(rval[t]))
+        gap = rval[t] - rval[t + 1] > 10 * tt and (t == 0 or rval[t - 1] - rval[t] > 10 * tt)
+        if gap:
+            assert sel[t] == ridx[t], (it, t, sel[t], ridx[t])
+        else:
+            assert abs(acq[sel[t]] - rval[t]) <= 2 * tt, (it, t)
