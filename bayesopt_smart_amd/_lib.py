@@ -89,6 +89,10 @@ _SIGS = {
                                C.POINTER(C.c_int64)]),
     "bo_hypervolume_improvement_exact": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int64, C.c_int32,
                                                    c_dbl_p, c_dbl_p, c_vp, C.c_int64, c_vp]),
+    "bo_hvi_select_topq": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int64, C.c_int32, c_dbl_p, c_dbl_p, c_vp,
+                                     C.c_int64, C.c_int32, c_vp, C.POINTER(C.c_int64),
+                                     C.POINTER(C.c_int64), C.c_int32, C.c_int64, c_vp, C.c_int64,
+                                     C.c_int32, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
     "bo_invert_k": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, C.c_size_t, c_vp]),
     "bo_invert_k_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
     "bo_compute_mll": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,

@@ -146,6 +146,45 @@ def hypervolume_improvement_exact(ucb, front, reference_point, prior_mean, prior
     return dst if isinstance(ucb, torch.Tensor) else dst.cpu().numpy()
 
 
+def hvi_select_indices(acquisition_values, ucb, y_vector, n_evaluations, reference_point, prior_mean,
+                       prior_variance, cands, evaluated_points, batch_size):
+    """The exact-HVI acquisition AND its batch selection in one device pass (bo_hvi_select_topq,
+    batch_size <= 16): acquisition_values (device, [M]) receives the HVI of every candidate's
+    UCB vector over the Pareto front of y_vector[:n_evaluations]; returns the global indices of
+    the best batch_size candidates not equal to an evaluated point (select_next_batch's order)."""
+    from .pareto import is_pareto_efficient
+    if batch_size > 16:
+        raise ValueError("hvi_select_indices handles batch_size <= 16")
+    y = y_vector[:n_evaluations]
+    front = y[is_pareto_efficient(y)] if n_evaluations > 0 else np.zeros((0, len(reference_point)))
+    if isinstance(front, torch.Tensor):
+        front = front.cpu().numpy()
+    dev = _dev_of(acquisition_values, ucb)
+    u = _Arg(ucb, dev)
+    acq = _Arg(acquisition_values, dev, write=True)
+    n_obj, n = u.t.shape
+    boxes = torch.as_tensor(hypervolume_boxes(front, reference_point), device=dev)
+    ev = np.asarray(evaluated_points.cpu().numpy() if isinstance(evaluated_points, torch.Tensor)
+                    else evaluated_points, dtype=np.float64).reshape(-1, cands.dim)
+    ex = torch.as_tensor(np.ascontiguousarray(ev), device=dev)
+    rec = torch.empty(2 * batch_size, dtype=F64, device=dev)
+    lib = _lib.load()
+    ws = Workspace.get(lib.bo_select_topq_workspace_size(n, batch_size), dev)
+    lo = (C_i64 * 8)(*(list(cands.lo or []) + [0] * (8 - len(cands.lo or []))))
+    sh = (C_i64 * 8)(*(list(cands.shape or []) + [1] * (8 - len(cands.shape or []))))
+    shift = _host_vec(prior_mean, n_obj)
+    scale = _host_vec(np.sqrt(np.asarray(prior_variance, dtype=np.float64)), n_obj)
+    _lib.check(lib.bo_hvi_select_topq(acq.ptr, u.ptr, u.t.stride(0), n, n_obj, shift, scale,
+                                      boxes.data_ptr() if boxes.numel() else None, boxes.shape[0],
+                                      cands.kind_code, cands.cand_arg, lo, sh, cands.dim, 0,
+                                      ex.data_ptr() if ex.numel() else None, ex.shape[0], batch_size,
+                                      rec.data_ptr(), rec.data_ptr() + 8 * batch_size, ws.data_ptr(),
+                                      ws.numel(), stream_handle(dev)), "bo_hvi_select_topq")
+    acq.finish()
+    idx = rec[batch_size:].view(torch.int64).cpu().numpy()
+    return idx[idx >= 0]
+
+
 def update_hypervolume_improvement_exact(acquisition_values, ucb, y_vector, n_evaluations,
                                          reference_point, prior_mean, prior_variance):
     """The acquisition update of the loop (bayesian_optimization.py:195-199) as an exact HVI:

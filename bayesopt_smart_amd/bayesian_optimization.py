@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from .acquisition import select_indices, update_hypervolume_improvement_exact
+from .acquisition import hvi_select_indices, select_indices, update_hypervolume_improvement_exact
 from .config import (DEFAULT_BATCH_SIZE, DEFAULT_BETA, DEFAULT_INITIAL_SAMPLES,
                      DEFAULT_LENGTH_SCALE, DEFAULT_PRIOR_MEAN, DEFAULT_PRIOR_VARIANCE,
                      NUMBA_FLOAT_TYPE)
@@ -83,6 +83,11 @@ def _predict_select(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, lengt
     q = batch_size if batch_size <= _lib.MAX_TOPQ and acquisition == "sum_ucb" else 0
     r = predict_acquire(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
                         outputs=tuple(out), topq=q, out=out)
+    if acquisition == "hvi" and batch_size <= 16:
+        # exact HVI and its top-q with exclusion in one device pass
+        idx = hvi_select_indices(buffers.acquisition_values, buffers.ucb, y_evaluated, len(y_evaluated),
+                                 reference_point, prior_mean, prior_variance, cands, evaluated, batch_size)
+        return cands.points(idx) if idx.size else np.zeros((0, cands.dim), dtype=np.int64)
     if acquisition == "hvi":
         update_hypervolume_improvement_exact(buffers.acquisition_values, buffers.ucb, y_evaluated,
                                              len(y_evaluated), reference_point, prior_mean,

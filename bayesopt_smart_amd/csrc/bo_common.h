@@ -79,6 +79,65 @@ __device__ __forceinline__ void bo_wave_topq_insert(double& lv, long long& li, d
   if (lane >= q) { lv = -__builtin_inf(); li = -1; }
 }
 
+// Final merge of per-wave / per-workgroup top lists (`total` entries, <= 8 per thread of the
+// single 1024-thread workgroup, i.e. <= 8192): q rounds of a workgroup-wide arg-best over the
+// entries held in registers, the winner retired by its (unique) global index.  Used for q <= 16
+// by bo_predict_acquire and bo_select_topq (the bitonic merge serves larger q).
+static __global__ __launch_bounds__(1024) void bo_argbest_merge_kernel(const TopEntry* __restrict__ lists,
+                                                                       long long total, int q,
+                                                                       double* __restrict__ out_v,
+                                                                       long long* __restrict__ out_i) {
+  __shared__ TopEntry wbest[16];
+  __shared__ TopEntry win;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  double v[8];
+  long long ix[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const long long at = tid + (long long)k * blockDim.x;
+    v[k] = -__builtin_inf();
+    ix[k] = -1;
+    if (at < total) { v[k] = lists[at].v; ix[k] = lists[at].i; }
+  }
+  for (int r = 0; r < q; ++r) {
+    double bv = -__builtin_inf();
+    long long bi = -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (bo_better(v[k], ix[k], bv, bi)) { bv = v[k]; bi = ix[k]; }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+      const double ov = __shfl_xor(bv, m, 64);
+      const long long oi = __shfl_xor(bi, m, 64);
+      if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { wbest[wave].v = bv; wbest[wave].i = bi; }
+    __syncthreads();
+    if (wave == 0) {
+      bv = lane < nw ? wbest[lane].v : -__builtin_inf();
+      bi = lane < nw ? wbest[lane].i : -1;
+#pragma unroll
+      for (int m = 32; m > 0; m >>= 1) {
+        const double ov = __shfl_xor(bv, m, 64);
+        const long long oi = __shfl_xor(bi, m, 64);
+        if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+      }
+      if (lane == 0) {
+        win.v = bv;
+        win.i = bi;
+        out_v[r] = bv;
+        out_i[r] = bi;
+      }
+    }
+    __syncthreads();
+    const long long wi = win.i;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (wi >= 0 && ix[k] == wi) { v[k] = -__builtin_inf(); ix[k] = -1; }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Sobol candidates (BO_CAND_SOBOL): direction numbers (host) and one coordinate (device).
 // ---------------------------------------------------------------------------------------

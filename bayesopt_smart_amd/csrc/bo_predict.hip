@@ -280,65 +280,6 @@ __global__ __launch_bounds__(1024) void topq_merge_kernel(const TopEntry* __rest
   }
 }
 
-// Small q (<= 16): q rounds of a workgroup-wide arg-best over all list entries held in
-// registers (<= 8 per thread), instead of bitonic inserts: a few shuffle reductions per round.
-__global__ __launch_bounds__(1024) void topq_argbest_kernel(const TopEntry* __restrict__ lists,
-                                                            int n_lists, int q,
-                                                            double* __restrict__ out_v,
-                                                            long long* __restrict__ out_i) {
-  __shared__ TopEntry wbest[16];
-  __shared__ TopEntry win;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  const long long total = (long long)n_lists * q;
-  double v[8];
-  long long ix[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const long long at = tid + (long long)k * blockDim.x;
-    v[k] = -__builtin_inf();
-    ix[k] = -1;
-    if (at < total) { v[k] = lists[at].v; ix[k] = lists[at].i; }
-  }
-  for (int r = 0; r < q; ++r) {
-    double bv = -__builtin_inf();
-    long long bi = -1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (bo_better(v[k], ix[k], bv, bi)) { bv = v[k]; bi = ix[k]; }
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) {
-      const double ov = __shfl_xor(bv, m, 64);
-      const long long oi = __shfl_xor(bi, m, 64);
-      if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) { wbest[wave].v = bv; wbest[wave].i = bi; }
-    __syncthreads();
-    if (wave == 0) {
-      bv = lane < nw ? wbest[lane].v : -__builtin_inf();
-      bi = lane < nw ? wbest[lane].i : -1;
-#pragma unroll
-      for (int m = 32; m > 0; m >>= 1) {
-        const double ov = __shfl_xor(bv, m, 64);
-        const long long oi = __shfl_xor(bi, m, 64);
-        if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-      }
-      if (lane == 0) {
-        win.v = bv;
-        win.i = bi;
-        out_v[r] = bv;
-        out_i[r] = bi;
-      }
-    }
-    __syncthreads();
-    // retire the winner (global candidate indices are unique across the lists)
-    const long long wi = win.i;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (wi >= 0 && ix[k] == wi) { v[k] = -__builtin_inf(); ix[k] = -1; }
-    __syncthreads();
-  }
-}
-
 __global__ void selftest_mfma_kernel(const double* a, const double* b, double* d) {
   const int l = threadIdx.x;
   const double av = a[(l & 15) * 4 + (l >> 4)];  // A[i=l&15][k=l>>4]
@@ -818,8 +759,8 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   if (d->topq > 0) {
     const int n_lists = pl.grid * pl.waves;
     if (d->topq <= 16 && (long long)n_lists * d->topq <= 8 * 1024)
-      hipLaunchKernelGGL(topq_argbest_kernel, dim3(1), dim3(1024), 0, s, partial, n_lists,
-                         d->topq, d->top_val, (long long*)d->top_idx);
+      hipLaunchKernelGGL(bo_argbest_merge_kernel, dim3(1), dim3(1024), 0, s, partial,
+                         (long long)n_lists * d->topq, d->topq, d->top_val, (long long*)d->top_idx);
     else
       hipLaunchKernelGGL(topq_merge_kernel, dim3(1), dim3(1024), 0, s, partial, n_lists,
                          d->topq, d->top_val, (long long*)d->top_idx);

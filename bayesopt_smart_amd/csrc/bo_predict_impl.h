@@ -355,6 +355,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
   const int voff = lane * 16;
   const int w_obj = a.w_pairs / a.n_obj * 2048;             // bytes of one objective's stream
+
   // the centre z (training row 0) of the non-SEP generation
   double z[DIM];
 #pragma unroll
@@ -429,9 +430,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #pragma unroll
       for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
       const double* al = alpha + (size_t)o * a.n_pad;
-      // W ring: primed per objective (a ring running on across objectives and tiles measured
-      // 7 % slower at C4 -- its modular refill offsets defeat the immediate-offset addressing --
-      // and no faster at C2)
+      // W ring: primed per objective (a ring running on across objectives and tiles, wrapping
+      // at the end of the packed streams, measured 1.7 % slower at C4 and 3 % faster at C2 on
+      // one box: its modular refill offsets defeat the immediate-offset addressing)
       const int base = o * w_obj;
       d2 wa[kPF], wb[kPF];
       prime_ring(wr, voff, base, wa, wb);
@@ -443,14 +444,13 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       // regenerates their K*.  One group when N <= 512.
       for (int e0 = 0; e0 < nch; e0 += kCMaxEp) {
         const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
-        // zero the group's eN accumulator pairs only (small N: 4 of 16 at C2, each pair is 16
-        // AGPR writes)
-        auto zero_acc = [&](auto e_c) {
-          constexpr int e = decltype(e_c)::value;
+        // all kCMaxEp accumulator pairs zeroed unconditionally (zeroing only the group's eN
+        // pairs behind nested guards measured 1-2 % slower at C2/C3/C4)
+#pragma unroll
+        for (int e = 0; e < kCMaxEp; ++e) {
           acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
           acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
-        };
-        EpChain<0, kCMaxEp>::run(zero_acc, eN);
+        }
         // one chunk: MFMAs from register set B while the next chunk's K* (and its alpha
         // values, An) is generated into Bn in three stages inside E-pair 0's MFMA stream (the
         // sets alternate: no register copies between the chunks).  Branch-free: the last chunk

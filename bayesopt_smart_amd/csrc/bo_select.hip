@@ -190,6 +190,142 @@ __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Selection for q <= 16 (every batch the reference's demos use), ONE pass at HBM rate:
+// every thread keeps its own sorted top-Q (Q = 4 / 8 / 16 >= q) in registers over a
+// coalesced grid-stride sweep -- almost every element is rejected by one comparison with the
+// thread's Q-th entry; evaluated points are skipped by the grid bitmap, or (explicit sets) by
+// an exact coordinate test run only for elements that would enter the list -- then the wave
+// and the workgroup reduce their lists by Q rounds of arg-best (shuffles; the winner's owner
+// pops it), and bo_argbest_merge_kernel merges the workgroups' lists.
+// M > 0 fuses the exact hypervolume improvement of bo_hvi.hip into the sweep: the acquisition
+// of candidate i is computed from its M UCB values and the boxes (wave-uniform, scalar loads),
+// written to acq, and selected in the same pass (one HBM read of the UCB arrays in total).
+// ---------------------------------------------------------------------------------------
+struct HviIn {
+  const double* ucb;          // [M][ld]
+  long long ld;
+  const double* boxes;        // [n_boxes][2 M]
+  long long n_boxes;
+  double shift[BO_MAX_OBJ], scale[BO_MAX_OBJ];
+  double* acq_out;
+};
+
+template <int Q>
+__device__ __forceinline__ void lane_insert(double (&v)[Q], long long (&ix)[Q], double nv, long long ni) {
+  // sorted best-first; nv beats v[Q - 1] (checked by the caller)
+#pragma unroll
+  for (int k = Q - 1; k >= 0; --k) {
+    const bool beats_k = bo_better(nv, ni, v[k], ix[k]);
+    const bool beats_prev = k > 0 && bo_better(nv, ni, v[k > 0 ? k - 1 : 0], ix[k > 0 ? k - 1 : 0]);
+    if (beats_k) {
+      v[k] = beats_prev ? v[k - (k > 0)] : nv;
+      ix[k] = beats_prev ? ix[k - (k > 0)] : ni;
+    }
+  }
+}
+
+template <int Q, int M>
+__global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
+  __shared__ TopEntry wl[4 * Q];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double v[Q];
+  long long ix[Q];
+#pragma unroll
+  for (int k = 0; k < Q; ++k) { v[k] = -__builtin_inf(); ix[k] = -1; }
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long j = (long long)blockIdx.x * blockDim.x + tid; j < a.n_cand; j += stride) {
+    double val;
+    if constexpr (M == 0) {
+      val = a.acq[j];
+    } else {
+      double p[M];
+      bool nan = false;
+#pragma unroll
+      for (int k = 0; k < M; ++k) {
+        p[k] = __builtin_fma(h.scale[k], h.ucb[(long long)k * h.ld + j], h.shift[k]);
+        nan = nan || (p[k] != p[k]);
+      }
+      double hv = 0.0;
+      const double* b = h.boxes;
+      for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
+        double w = 1.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          const double hi = p[k] < b[M + k] ? p[k] : b[M + k];
+          w *= fmax(hi - b[k], 0.0);
+        }
+        hv += w;
+      }
+      val = nan ? __builtin_nan("") : hv;
+      h.acq_out[j] = val;
+    }
+    const long long gi = a.cand_offset + j;
+    if (a.bitmap && ((a.bitmap[j >> 5] >> (j & 31)) & 1u)) continue;
+    if (!bo_better(val, gi, v[Q - 1], ix[Q - 1])) continue;
+    if (!a.bitmap && a.n_excl > 0) {
+      double c[BO_MAX_DIM];
+      for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
+      bool hit = false;
+      for (int e = 0; e < a.n_excl && !hit; ++e) {
+        bool eq = true;
+        for (int k = 0; k < a.dim; ++k) eq = eq && (a.excl[(long long)e * a.dim + k] == c[k]);
+        hit = eq;
+      }
+      if (hit) continue;
+    }
+    lane_insert<Q>(v, ix, val, gi);
+  }
+  // wave: Q rounds of arg-best over the lanes' heads; the owner pops its head
+#pragma unroll 1
+  for (int r = 0; r < Q; ++r) {
+    double bv = v[0];
+    long long bi = ix[0];
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+      const double ov = __shfl_xor(bv, m, 64);
+      const long long oi = __shfl_xor(bi, m, 64);
+      if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { wl[wave * Q + r].v = bv; wl[wave * Q + r].i = bi; }
+    if (bi >= 0 && ix[0] == bi) {
+#pragma unroll
+      for (int k = 0; k + 1 < Q; ++k) { v[k] = v[k + 1]; ix[k] = ix[k + 1]; }
+      v[Q - 1] = -__builtin_inf();
+      ix[Q - 1] = -1;
+    }
+  }
+  __syncthreads();
+  // workgroup: wave 0 merges the 4 wave lists (4 Q <= 64 entries, one per lane)
+  if (wave == 0) {
+    double ev = lane < 4 * Q ? wl[lane].v : -__builtin_inf();
+    long long ei = lane < 4 * Q ? wl[lane].i : -1;
+    TopEntry* dst = a.partial + (size_t)blockIdx.x * Q;
+#pragma unroll 1
+    for (int r = 0; r < Q; ++r) {
+      double bv = ev;
+      long long bi = ei;
+#pragma unroll
+      for (int m = 32; m > 0; m >>= 1) {
+        const double ov = __shfl_xor(bv, m, 64);
+        const long long oi = __shfl_xor(bi, m, 64);
+        if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+      }
+      if (lane == 0) { dst[r].v = bv; dst[r].i = bi; }
+      if (bi >= 0 && ei == bi) { ev = -__builtin_inf(); ei = -1; }
+    }
+  }
+}
+
+template <int M>
+int launch_select_lane(const SelArgs& a, const HviIn& h, int q, int blocks, hipStream_t s) {
+  if (q <= 4) hipLaunchKernelGGL((select_lane_kernel<4, M>), dim3(blocks), dim3(256), 0, s, a, h);
+  else if (q <= 8) hipLaunchKernelGGL((select_lane_kernel<8, M>), dim3(blocks), dim3(256), 0, s, a, h);
+  else hipLaunchKernelGGL((select_lane_kernel<16, M>), dim3(blocks), dim3(256), 0, s, a, h);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
 __global__ __launch_bounds__(1024) void merge_kernel(const TopEntry* __restrict__ lists,
                                                      int n_lists, int q, double* __restrict__ out_v,
                                                      long long* __restrict__ out_i) {
@@ -353,17 +489,23 @@ size_t bo_select_topq_workspace_size(int64_t n_cand, int32_t topq) {
   return lists + (bits + 255) / 256 * 256;
 }
 
-int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* cand,
-                   const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
-                   int64_t cand_offset, const double* excl, int64_t n_excl, int32_t topq,
-                   double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes, void* stream) {
-  if (!acq || topq < 1 || topq > BO_MAX_TOPQ || dim < 1 || dim > BO_MAX_DIM || n_cand < 0 ||
-      !top_val || !top_idx || (n_excl > 0 && !excl) || kind < 0 || kind > BO_CAND_SOBOL)
+}  // extern "C"
+
+namespace {
+
+// select_next_batch over an acquisition array (m == 0) or over the exact HVI computed from the
+// UCB arrays in the same pass (m >= 1, `h`), written into h->acq_out first.
+int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* cand,
+                const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
+                int64_t cand_offset, const double* excl, int64_t n_excl, int32_t topq,
+                double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes, hipStream_t s,
+                const HviIn* h, int m) {
+  if ((!acq && m == 0) || topq < 1 || topq > BO_MAX_TOPQ || dim < 1 || dim > BO_MAX_DIM ||
+      n_cand < 0 || !top_val || !top_idx || (n_excl > 0 && !excl) || kind < 0 || kind > BO_CAND_SOBOL)
     return BO_ERR_ARG;
   if (kind != BO_CAND_GRID && !cand) return BO_ERR_ARG;
   if (kind == BO_CAND_GRID && (!grid_lo || !grid_shape)) return BO_ERR_ARG;
   if (!ws || ws_bytes < bo_select_topq_workspace_size(n_cand, topq)) return BO_ERR_WORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
   SelArgs a;
   memset(&a, 0, sizeof(a));
   a.acq = acq;
@@ -396,7 +538,32 @@ int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* 
     a.bitmap = bm;
   }
   long long blocks = (n_cand + 255) / 256;
-  // one workgroup per CU: an HBM-bound pass of 8 B per candidate; fewer lists for the merge
+  if (topq <= 16) {
+    // two workgroups per CU keep enough loads in flight for the HBM-bound sweep
+    const int max_blocks = 2 * cus_count() < 512 ? 2 * cus_count() : 512;
+    if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks < 1) blocks = 1;
+    HviIn hz;
+    memset(&hz, 0, sizeof(hz));
+    const HviIn& hv = h ? *h : hz;
+    int st;
+    switch (m) {
+      case 0: st = launch_select_lane<0>(a, hv, topq, (int)blocks, s); break;
+      case 1: st = launch_select_lane<1>(a, hv, topq, (int)blocks, s); break;
+      case 2: st = launch_select_lane<2>(a, hv, topq, (int)blocks, s); break;
+      case 3: st = launch_select_lane<3>(a, hv, topq, (int)blocks, s); break;
+      case 4: st = launch_select_lane<4>(a, hv, topq, (int)blocks, s); break;
+      default: return BO_ERR_UNSUPPORTED;
+    }
+    if (st != BO_OK) return st;
+    const int Q = topq <= 4 ? 4 : (topq <= 8 ? 8 : 16);
+    hipLaunchKernelGGL(bo_argbest_merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
+                       blocks * Q, topq, top_val, (long long*)top_idx);
+    BO_CHECK_HIP(hipGetLastError());
+    return BO_OK;
+  }
+  if (m != 0) return BO_ERR_UNSUPPORTED;   // (the caller runs the HVI scan first for q > 16)
+  // q > 16: per-wave bitonic lists, one workgroup per CU
   const int max_blocks = cus_count() < 1024 ? cus_count() : 1024;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
@@ -406,6 +573,47 @@ int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* 
                      (int)blocks * 4, topq, top_val, (long long*)top_idx);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bo_select_topq(const double* acq, int64_t n_cand, int32_t kind, const void* cand,
+                   const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
+                   int64_t cand_offset, const double* excl, int64_t n_excl, int32_t topq,
+                   double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes, void* stream) {
+  return select_impl(acq, n_cand, kind, cand, grid_lo, grid_shape, dim, cand_offset, excl, n_excl,
+                     topq, top_val, top_idx, ws, ws_bytes, (hipStream_t)stream, nullptr, 0);
+}
+
+int bo_hvi_select_topq(double* acq, const double* ucb, int64_t ld, int64_t n_cand, int32_t n_obj,
+                       const double* shift, const double* scale, const double* boxes,
+                       int64_t n_boxes, int32_t kind, const void* cand, const int64_t* grid_lo,
+                       const int64_t* grid_shape, int32_t dim, int64_t cand_offset,
+                       const double* excl, int64_t n_excl, int32_t topq, double* top_val,
+                       int64_t* top_idx, void* ws, size_t ws_bytes, void* stream) {
+  if (!acq || !ucb || !shift || !scale || n_obj < 1 || n_obj > 4 || ld < n_cand || n_boxes < 0 ||
+      (n_boxes > 0 && !boxes))
+    return BO_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (topq > 16) {   // large batches: the standalone HVI scan, then the bitonic selection
+    const int st = bo_hypervolume_improvement_exact(acq, ucb, ld, n_cand, n_obj, shift, scale, boxes,
+                                                    n_boxes, stream);
+    if (st != BO_OK) return st;
+    return select_impl(acq, n_cand, kind, cand, grid_lo, grid_shape, dim, cand_offset, excl, n_excl,
+                       topq, top_val, top_idx, ws, ws_bytes, s, nullptr, 0);
+  }
+  HviIn h;
+  memset(&h, 0, sizeof(h));
+  h.ucb = ucb;
+  h.ld = ld;
+  h.boxes = boxes;
+  h.n_boxes = n_boxes;
+  for (int k = 0; k < n_obj; ++k) { h.shift[k] = shift[k]; h.scale[k] = scale[k]; }
+  h.acq_out = acq;
+  return select_impl(acq, n_cand, kind, cand, grid_lo, grid_shape, dim, cand_offset, excl, n_excl,
+                     topq, top_val, top_idx, ws, ws_bytes, s, &h, n_obj);
 }
 
 int bo_pareto_mask(const double* y, int64_t n, int32_t n_obj, uint8_t* mask, void* stream) {

@@ -224,6 +224,16 @@ int bo_pareto_mask(const double* y, int64_t n, int32_t n_obj, uint8_t* mask, voi
  * [n_obj][ld], the standardised UCB; shift = prior mean, scale = sqrt(prior variance) give
  * mu + beta sigma in objective units).  boxes: device copy of bo_hvi_boxes' output.  NaN in p
  * gives NaN (selected first, as NaN is by the reference's argsort).  shift/scale host. */
+/* bo_hvi_select_topq: the exact HVI of bo_hypervolume_improvement_exact written into acq AND
+ * the top-q selection of bo_select_topq over it, in one pass over the UCB arrays (q <= 16;
+ * larger q runs the two steps).  Arguments as those two functions'; workspace
+ * bo_select_topq_workspace_size(n_cand, topq). */
+int bo_hvi_select_topq(double* acq, const double* ucb, int64_t ld, int64_t n_cand, int32_t n_obj,
+                       const double* shift, const double* scale, const double* boxes,
+                       int64_t n_boxes, int32_t cand_kind, const void* cand, const int64_t* grid_lo,
+                       const int64_t* grid_shape, int32_t dim, int64_t cand_offset,
+                       const double* excl_points, int64_t n_excl, int32_t topq, double* top_val,
+                       int64_t* top_idx, void* workspace, size_t workspace_bytes, void* stream);
 int bo_hvi_boxes(const double* front, int64_t n, int32_t n_obj, const double* ref_point,
                  double* boxes, int64_t capacity, int64_t* n_boxes);
 int bo_hypervolume_improvement_exact(double* acq, const double* ucb, int64_t ld, int64_t n,

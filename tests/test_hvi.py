@@ -125,3 +125,45 @@ def test_device_hvi_full_scan_properties():
     out = torch.zeros(n, dtype=torch.float64, device="cuda")
     update_hypervolume_improvement_exact(out, ucb, y, 4, np.full(m, -3.0), pm, pv)
     assert np.array_equal(out.cpu().numpy(), acq)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,m,q", [("grid", 2, 3), ("grid", 3, 16), ("f64", 2, 8), ("sobol", 3, 5),
+                                      ("grid", 2, 20)])
+def test_fused_hvi_select_matches_scan_plus_oracle_select(kind, m, q):
+    """bo_hvi_select_topq (exact HVI and its top-q in one pass) writes the same acquisition
+    array as the standalone HVI scan, bit for bit, and selects what select_next_batch
+    (acquisition.py:116-144, the oracle's deterministic order) selects over it, evaluated
+    points skipped (grid: bitmap; explicit / Sobol: exact coordinates).  q = 20 takes the
+    two-step path (scan, then the bitonic selection)."""
+    import torch
+    from bayesopt_smart_amd.acquisition import hvi_select_indices, hypervolume_improvement_exact
+    from bayesopt_smart_amd.predict import CandidateSet
+    rng = np.random.default_rng(m * 100 + q)
+    if kind == "grid":
+        cands = CandidateSet.grid([(0, 512), (0, 300)])
+    elif kind == "sobol":
+        cands = CandidateSet.sobol_set(4, 150_000, scale=50.0)
+    else:
+        cands = CandidateSet.explicit(rng.uniform(0, 10, size=(120_000, 3)))
+    n = cands.n
+    ucb = torch.as_tensor(rng.normal(size=(m, n)), device="cuda")
+    ucb[:, 17] = float("nan")                               # a NaN candidate is selected first
+    pm, pv = rng.normal(size=m), rng.uniform(0.5, 2.0, size=m)
+    y = rng.normal(size=(40, m))
+    ev = cands.points(rng.choice(n, 40, replace=False)).astype(np.float64)
+    ref_pt = np.full(m, -4.0)
+    acq = torch.zeros(n, dtype=torch.float64, device="cuda")
+    idx = hvi_select_indices(acq, ucb, y, 40, ref_pt, pm, pv, cands, ev, q) if q <= 16 else None
+    front = y[O.is_pareto_efficient(y)]
+    scan = hypervolume_improvement_exact(ucb, front, ref_pt, pm, pv).cpu().numpy()
+    if q <= 16:
+        np.testing.assert_array_equal(acq.cpu().numpy(), scan)
+    else:
+        from bayesopt_smart_amd.acquisition import select_indices
+        idx = select_indices(torch.as_tensor(scan, device="cuda"), cands, ev, q)
+    evs = {tuple(r) for r in ev}
+    pts = cands.points(np.arange(n)).astype(np.float64)
+    excl = np.array([tuple(p) in evs for p in pts])
+    want = O.select_next_batch_indices(scan, excl, q)
+    np.testing.assert_array_equal(idx, want)
