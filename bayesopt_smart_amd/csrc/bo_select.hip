@@ -234,47 +234,62 @@ __global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
 #pragma unroll
   for (int k = 0; k < Q; ++k) { v[k] = -__builtin_inf(); ix[k] = -1; }
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long j = (long long)blockIdx.x * blockDim.x + tid; j < a.n_cand; j += stride) {
-    double val;
-    if constexpr (M == 0) {
-      val = a.acq[j];
-    } else {
-      double p[M];
-      bool nan = false;
+  // U elements per thread and sweep step, all loaded before any is processed (the loads of a
+  // step are in flight together; the loop body alone would expose one latency per element)
+  constexpr int U = 4;
+  for (long long j0 = (long long)blockIdx.x * blockDim.x + tid; j0 < a.n_cand; j0 += U * stride) {
+    double val[U];
+    uint32_t bits[U];
 #pragma unroll
-      for (int k = 0; k < M; ++k) {
-        p[k] = __builtin_fma(h.scale[k], h.ucb[(long long)k * h.ld + j], h.shift[k]);
-        nan = nan || (p[k] != p[k]);
-      }
-      double hv = 0.0;
-      const double* b = h.boxes;
-      for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
-        double w = 1.0;
+    for (int u = 0; u < U; ++u) {
+      const long long j = j0 + u * stride;
+      const bool in = j < a.n_cand;
+      bits[u] = (in && a.bitmap) ? a.bitmap[j >> 5] : 0u;
+      if constexpr (M == 0) {
+        val[u] = in ? a.acq[j] : 0.0;
+      } else {
+        double p[M];
+        bool nan = false;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
-          const double hi = p[k] < b[M + k] ? p[k] : b[M + k];
-          w *= fmax(hi - b[k], 0.0);
+          p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
+          nan = nan || (p[k] != p[k]);
         }
-        hv += w;
+        double hv = 0.0;
+        const double* b = h.boxes;
+        for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
+          double w = 1.0;
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            const double hi = p[k] < b[M + k] ? p[k] : b[M + k];
+            w *= fmax(hi - b[k], 0.0);
+          }
+          hv += w;
+        }
+        val[u] = nan ? __builtin_nan("") : hv;
+        if (in) h.acq_out[j] = val[u];
       }
-      val = nan ? __builtin_nan("") : hv;
-      h.acq_out[j] = val;
     }
-    const long long gi = a.cand_offset + j;
-    if (a.bitmap && ((a.bitmap[j >> 5] >> (j & 31)) & 1u)) continue;
-    if (!bo_better(val, gi, v[Q - 1], ix[Q - 1])) continue;
-    if (!a.bitmap && a.n_excl > 0) {
-      double c[BO_MAX_DIM];
-      for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
-      bool hit = false;
-      for (int e = 0; e < a.n_excl && !hit; ++e) {
-        bool eq = true;
-        for (int k = 0; k < a.dim; ++k) eq = eq && (a.excl[(long long)e * a.dim + k] == c[k]);
-        hit = eq;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long j = j0 + u * stride;
+      if (j >= a.n_cand) break;
+      const long long gi = a.cand_offset + j;
+      if ((bits[u] >> (j & 31)) & 1u) continue;
+      if (!bo_better(val[u], gi, v[Q - 1], ix[Q - 1])) continue;
+      if (!a.bitmap && a.n_excl > 0) {
+        double c[BO_MAX_DIM];
+        for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
+        bool hit = false;
+        for (int e = 0; e < a.n_excl && !hit; ++e) {
+          bool eq = true;
+          for (int k = 0; k < a.dim; ++k) eq = eq && (a.excl[(long long)e * a.dim + k] == c[k]);
+          hit = eq;
+        }
+        if (hit) continue;
       }
-      if (hit) continue;
+      lane_insert<Q>(v, ix, val[u], gi);
     }
-    lane_insert<Q>(v, ix, val, gi);
   }
   // wave: Q rounds of arg-best over the lanes' heads; the owner pops its head
 #pragma unroll 1
@@ -389,6 +404,12 @@ __global__ __launch_bounds__(256) void pareto_kernel(const double* __restrict__ 
   if (i < n) mask[i] = dominated ? 0 : 1;
 }
 
+// partial lists: bitonic path <= 1024 workgroups x 4 waves x q; lane path <= 8192 entries
+size_t sel_lists_bytes(int topq) {
+  const size_t e = (size_t)1024 * 4 * (topq > 0 ? topq : 1);
+  return (e > 8192 ? e : 8192) * sizeof(TopEntry);
+}
+
 int cus_count() {
   static int cus = 0;
   if (!cus) {
@@ -484,7 +505,7 @@ int bo_update_hypervolume_improvement(double* acq, const double* ucb, int32_t n_
 }
 
 size_t bo_select_topq_workspace_size(int64_t n_cand, int32_t topq) {
-  const size_t lists = (size_t)1024 * 4 * (topq > 0 ? topq : 1) * sizeof(TopEntry);
+  const size_t lists = sel_lists_bytes(topq);
   const size_t bits = ((size_t)(n_cand > 0 ? n_cand : 0) + 31) / 32 * 4;
   return lists + (bits + 255) / 256 * 256;
 }
@@ -531,7 +552,7 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   a.excl = excl;
   a.partial = (TopEntry*)ws;
   if (kind == BO_CAND_GRID && n_excl > 0 && n_cand > 0) {
-    uint32_t* bm = (uint32_t*)((char*)ws + (size_t)1024 * 4 * topq * sizeof(TopEntry));
+    uint32_t* bm = (uint32_t*)((char*)ws + sel_lists_bytes(topq));
     BO_CHECK_HIP(hipMemsetAsync(bm, 0, ((size_t)n_cand + 31) / 32 * 4, s));
     hipLaunchKernelGGL(excl_bitmap_kernel, dim3((unsigned)((n_excl + 255) / 256)), dim3(256), 0, s, bm, a);
     BO_CHECK_HIP(hipGetLastError());
@@ -539,8 +560,11 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   }
   long long blocks = (n_cand + 255) / 256;
   if (topq <= 16) {
-    // two workgroups per CU keep enough loads in flight for the HBM-bound sweep
-    const int max_blocks = 2 * cus_count() < 512 ? 2 * cus_count() : 512;
+    // up to 8 workgroups per CU keep the HBM-bound sweep's loads in flight; the final arg-best
+    // merge takes <= 8192 list entries (blocks x Q)
+    const int Qb = topq <= 4 ? 4 : (topq <= 8 ? 8 : 16);
+    const int cap = 8192 / Qb < 8 * cus_count() ? 8192 / Qb : 8 * cus_count();
+    const int max_blocks = cap;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
     HviIn hz;
