@@ -93,6 +93,7 @@ _SIGS = {
                                      C.c_int64, C.c_int32, c_vp, C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int64), C.c_int32, C.c_int64, c_vp, C.c_int64,
                                      C.c_int32, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
+    "bo_box_volume_sum": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_dbl_p, c_vp, c_vp]),
     "bo_invert_k": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, C.c_size_t, c_vp]),
     "bo_invert_k_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
     "bo_compute_mll": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,

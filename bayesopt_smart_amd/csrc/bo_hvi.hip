@@ -75,6 +75,30 @@ __global__ __launch_bounds__(256) void hvi_exact_kernel(const HviArgs a) {
   }
 }
 
+// out[0] = sum over boxes [b0, b1) of prod_k max(0, min(upper_bk, ub_k) - lower_bk): the volume
+// of the boxes clipped to [., ub].  One workgroup, boxes strided over its threads, fixed-order
+// tree reduction (deterministic).
+__global__ __launch_bounds__(1024) void box_volume_kernel(const double* __restrict__ boxes, long long n_boxes,
+                                                          int m, HviArgs ub, double* __restrict__ out) {
+  __shared__ double red[1024];
+  double s = 0.0;
+  for (long long b = threadIdx.x; b < n_boxes; b += blockDim.x) {
+    double v = 1.0;
+    for (int k = 0; k < m; ++k) {
+      const double hi = boxes[b * 2 * m + m + k] < ub.shift[k] ? boxes[b * 2 * m + m + k] : ub.shift[k];
+      v *= fmax(hi - boxes[b * 2 * m + k], 0.0);
+    }
+    s += v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
 int launch_hvi(const HviArgs& a, int m, hipStream_t s) {
   long long blocks = (a.n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
@@ -195,6 +219,18 @@ int bo_hypervolume_improvement_exact(double* acq, const double* ucb, int64_t ld,
   a.n_boxes = n_boxes;
   for (int k = 0; k < n_obj; ++k) { a.shift[k] = shift[k]; a.scale[k] = scale[k]; }
   return launch_hvi(a, n_obj, (hipStream_t)stream);
+}
+
+int bo_box_volume_sum(const double* boxes, int64_t n_boxes, int32_t n_obj, const double* upper,
+                      double* out, void* stream) {
+  if (!out || !upper || n_obj < 1 || n_obj > 4 || n_boxes < 0 || (n_boxes > 0 && !boxes)) return BO_ERR_ARG;
+  HviArgs ub;
+  memset(&ub, 0, sizeof(ub));
+  for (int k = 0; k < n_obj; ++k) ub.shift[k] = upper[k];
+  hipLaunchKernelGGL(box_volume_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, boxes,
+                     (long long)n_boxes, n_obj, ub, out);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
 }
 
 }  // extern "C"

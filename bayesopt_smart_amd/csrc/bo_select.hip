@@ -560,11 +560,9 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   }
   long long blocks = (n_cand + 255) / 256;
   if (topq <= 16) {
-    // up to 8 workgroups per CU keep the HBM-bound sweep's loads in flight; the final arg-best
-    // merge takes <= 8192 list entries (blocks x Q)
-    const int Qb = topq <= 4 ? 4 : (topq <= 8 ? 8 : 16);
-    const int cap = 8192 / Qb < 8 * cus_count() ? 8192 / Qb : 8 * cus_count();
-    const int max_blocks = cap;
+    // two workgroups per CU (8 per CU measured slower: the per-workgroup list merges and the
+    // longer final merge outweigh the extra loads in flight); blocks x Q <= 8192 list entries
+    const int max_blocks = 2 * cus_count() < 512 ? 2 * cus_count() : 512;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
     HviIn hz;

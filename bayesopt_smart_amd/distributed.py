@@ -47,6 +47,47 @@ def exchange_topq(top_val, top_idx, q, group=None):
     return exchange_topq_rec(rec, q, group)
 
 
+def front_hypervolume(front, reference_point, group=None, device=None, partial=None):
+    """The hypervolume accumulator: HV of the Pareto front `front` (host [P, m], maximisation)
+    above `reference_point`, with the box decomposition of the region the front does not
+    dominate (bo_hvi_boxes) split across the ranks -- each rank sums its boxes' volume clipped
+    to the front's bounding box (bo_box_volume_sum on the device) and ONE all_reduce(SUM)
+    combines them: HV = prod_k (max_k f_k - r_k) - sum.  Identical on every rank.
+
+    The reference names a reference point for its "hypervolume improvement"
+    (bayesian_optimization.py:65, :425) but never computes a hypervolume: parity unpinned,
+    checked against the oracle's recursive-slicing HV (tests).  `partial(boxes, upper)` replaces
+    the device sum (CPU ranks in tests)."""
+    from .acquisition import hypervolume_boxes
+    r = np.asarray(reference_point, dtype=np.float64).ravel()
+    f = np.asarray(front, dtype=np.float64).reshape(-1, r.size)
+    keep = np.all(np.isfinite(f), axis=1) & np.all(f > r, axis=1)
+    f = f[keep]
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if f.shape[0] == 0:
+        return 0.0
+    upper = f.max(axis=0)
+    boxes = hypervolume_boxes(f, r)
+    off, cnt = shard_range(boxes.shape[0], rank, world)
+    mine = np.ascontiguousarray(boxes[off:off + cnt])
+    if partial is not None:
+        val = torch.tensor([float(partial(mine, upper))], dtype=torch.float64)
+    else:
+        import ctypes
+        from . import _lib
+        from .device import require_device, stream_handle
+        dev = require_device(device)
+        bd = torch.as_tensor(mine, device=dev)
+        val = torch.zeros(1, dtype=torch.float64, device=dev)
+        ub = (ctypes.c_double * r.size)(*upper.tolist())
+        _lib.check(_lib.load().bo_box_volume_sum(bd.data_ptr() if bd.numel() else None, mine.shape[0], r.size,
+                                                 ub, val.data_ptr(), stream_handle(dev)), "bo_box_volume_sum")
+    if world > 1:
+        dist.all_reduce(val, op=dist.ReduceOp.SUM, group=group)
+    return float(np.prod(upper - r) - val.item())
+
+
 def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
                             betas, q, outputs=("acq",), group=None, device=None, scorer=None):
     """Score this rank's shard of `cands` and return (local results, global top-q).

@@ -443,6 +443,12 @@ def main():
     kms, nl = ctypes.c_double(), ctypes.c_int()
     lib.bo_profile_stop(ctypes.byref(kms), ctypes.byref(nl))
     t_step = dt / args.steps
+    hv_front = None
+    if args.acq == "hvi":
+        # the hypervolume accumulator: the front's box decomposition split over the ranks, one
+        # all_reduce (RCCL) -- outside the timed region, reported beside the selection
+        from bayesopt_smart_amd.distributed import front_hypervolume
+        hv_front = front_hypervolume(front_y, ref_pt, device=dev)
     if world > 1:
         tt = torch.tensor([t_step, kms.value / max(nl.value, 1)], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -505,6 +511,9 @@ def main():
             torch.cuda.synchronize()
             hms = float(np.mean([a.elapsed_time(b) for a, b in hvi_ev[-args.steps:]]))
             hb = (8 * n_obj + 8) * per_rank
+            res["front_hypervolume"] = {"value": hv_front, "reference_point": ref_pt.tolist(),
+                                        "method": f"bo_box_volume_sum over this rank's share of the "
+                                                  f"{n_boxes[0]} boxes + all_reduce(SUM) over {world} rank(s)"}
             res["hvi_select"] = {"kernels": f"select_lane_kernel<{4 if q <= 4 else 8 if q <= 8 else 16}, {n_obj}> "
                                             "+ bo_argbest_merge_kernel (exact HVI + top-q, one pass)",
                                  "ms": hms, "n_boxes": n_boxes[0], "front_points": int(front_y.shape[0]),

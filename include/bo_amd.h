@@ -234,6 +234,14 @@ int bo_hvi_select_topq(double* acq, const double* ucb, int64_t ld, int64_t n_can
                        const int64_t* grid_shape, int32_t dim, int64_t cand_offset,
                        const double* excl_points, int64_t n_excl, int32_t topq, double* top_val,
                        int64_t* top_idx, void* workspace, size_t workspace_bytes, void* stream);
+/* bo_box_volume_sum: out[0] (device) = sum_b prod_k max(0, min(upper_bk, upper[k]) - lower_bk)
+ * over `boxes` (device, bo_hvi_boxes layout): the volume of the boxes clipped above at `upper`
+ * (host [n_obj]).  With the boxes of the region a front does NOT dominate and upper = the
+ * front's per-objective maximum, HV(front) = prod_k (upper_k - ref_k) - that volume; a rank's
+ * share of the boxes gives its partial sum for the all-reduce "hypervolume accumulator"
+ * (bayesopt_smart_amd/distributed.py).  Deterministic (one workgroup, fixed-order tree). */
+int bo_box_volume_sum(const double* boxes, int64_t n_boxes, int32_t n_obj, const double* upper,
+                      double* out, void* stream);
 int bo_hvi_boxes(const double* front, int64_t n, int32_t n_obj, const double* ref_point,
                  double* boxes, int64_t capacity, int64_t* n_boxes);
 int bo_hypervolume_improvement_exact(double* acq, const double* ucb, int64_t ld, int64_t n,

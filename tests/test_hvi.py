@@ -167,3 +167,16 @@ def test_fused_hvi_select_matches_scan_plus_oracle_select(kind, m, q):
     excl = np.array([tuple(p) in evs for p in pts])
     want = O.select_next_batch_indices(scan, excl, q)
     np.testing.assert_array_equal(idx, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [2, 3, 4])
+def test_device_front_hypervolume(m):
+    """bo_box_volume_sum through distributed.front_hypervolume (one rank): HV of the front
+    against the oracle's recursive-slicing hypervolume (parity unpinned by the reference)."""
+    from bayesopt_smart_amd.distributed import front_hypervolume
+    rng = np.random.default_rng(40 + m)
+    y = rng.normal(size=(25 if m == 4 else 80, m))
+    front = y[O.is_pareto_efficient(y)]
+    ref = O.hypervolume(front, np.full(m, -3.0))
+    assert front_hypervolume(front, np.full(m, -3.0)) == pytest.approx(ref, rel=1e-12)
