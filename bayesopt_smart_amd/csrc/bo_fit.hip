@@ -20,10 +20,12 @@
 //     blocks of L^-T (upper triangular) are skipped, so the whole inverse costs about 3/2 of a
 //     Cholesky of the 2N system's first half.
 //
-// Per 64-column step k: chol_panel_kernel factors the diagonal tile in LDS (one wave, one row per
-// lane) and solves the tiles below it (row substitution, one row per lane; 4 row blocks per
-// workgroup); chol_update_kernel applies A_pq -= L_pk L_qk^T to every live tile of the trailing
-// matrix with v_mfma_f64_16x16x4_f64 (64 x 64 x 64 per workgroup).  A non-positive or NaN pivot
+// A is stored COLUMN-major (element (i, j) of the lower triangle at j * Na + i), so that the
+// row-per-lane accesses of the panel kernel and the row-contiguous tile loads of the update are
+// coalesced.  Per 64-column step k: chol_panel_kernel factors the diagonal tile (one wave, one
+// row per lane) and solves the tiles below it (row substitution, one row per lane; 4 row blocks
+// per workgroup); chol_update_kernel applies A_pq -= L_pk L_qk^T to every live tile of the
+// trailing matrix with v_mfma_f64_16x16x4_f64 (64 x 64 x 64 per workgroup).  A non-positive or NaN pivot
 // sets the objective's status (compute_mll: BO_ERR_NOT_PD = LinAlgError, as cholesky raises at
 // :214; invert_k: the LU fallback).  Sizes are not capped: the workspace is n_obj (N + 64)^2
 // doubles (MLL) or n_obj (2 N_p)^2 (inverse).
@@ -53,7 +55,8 @@ struct Aug {
 };
 
 // --------------------------------------------------------------------------- init
-// Lower triangle of the augmented matrix, per objective (blockIdx.y), row i = blockIdx.x:
+// Lower triangle of the augmented matrix, per objective (blockIdx.y), column j = blockIdx.x,
+// rows i >= j over the threads (coalesced column-major writes):
 //   i, j < N:           MLL: v / pv + 1e-8 d_ij with v = pv exp(-0.5 |x_i - x_j|^2 / ls^2) exactly
 //                       as update_k (numba_kernels.py:352-361), also written to the caller's
 //                       kernel_matrix (both triangles, the reference rebuilds it in compute_mll);
@@ -66,11 +69,11 @@ __global__ __launch_bounds__(256) void aug_init_kernel(double* __restrict__ A, A
                                                       const double* __restrict__ ycv, FitParams p,
                                                       int gram) {
   const int o = blockIdx.y;
-  const long long i = blockIdx.x;
+  const long long j = blockIdx.x;
   const long long np_ = (long long)g.nbt * NB;
   double* Ao = A + (long long)o * g.Na * g.Na;
   double* ko = km + (long long)o * ld * ld;
-  for (long long j = threadIdx.x; j <= i; j += blockDim.x) {
+  for (long long i = j + threadIdx.x; i < g.Na; i += blockDim.x) {
     double v = 0.0;
     if (i < np_) {
       if (i < g.n && j < g.n) {
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(256) void aug_init_kernel(double* __restrict__ A, A
       if (g.ident) v = (r == j && j < g.n) ? 1.0 : 0.0;
       else v = (r == 0 && j < g.n) ? ycv[(long long)o * g.n + j] : 0.0;
     }
-    Ao[i * g.Na + j] = v;
+    Ao[j * g.Na + i] = v;
   }
 }
 
@@ -151,15 +154,16 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
                                                         int* __restrict__ status) {
   __shared__ double L[NB][NB + 1];
   __shared__ double col[NB];
+  __shared__ double rdiag[NB];
   const int o = blockIdx.y;
   double* Ao = A + (long long)o * g.Na * g.Na;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long k0 = (long long)k * NB;
   if (wave == 0) {
     double a[NB];
-    const double* src = Ao + (k0 + lane) * g.Na + k0;
+    const double* src = Ao + k0 * g.Na + k0 + lane;       // (k0 + lane, k0 + t) at src[t Na]
 #pragma unroll
-    for (int t = 0; t < NB; ++t) a[t] = t <= lane ? src[t] : 0.0;
+    for (int t = 0; t < NB; ++t) a[t] = t <= lane ? src[t * g.Na] : 0.0;
     // a[t > lane] is scratch: it only ever receives updates, never feeds a real entry
     bool bad = false;
 #pragma unroll
@@ -167,9 +171,11 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
       const double piv = rdlane(a[j], j);
       bad = bad || !(piv > 0.0);             // potrf: ajj <= 0 or NaN -> not positive definite
       const double d = sqrt(piv);
-      const double lj = lane == j ? d : (lane > j ? a[j] / d : 0.0);
+      const double rd = 1.0 / d;               // wave-uniform: one reciprocal per column
+      const double lj = lane == j ? d : (lane > j ? a[j] * rd : 0.0);
       a[j] = lj;
       col[lane] = lj;
+      if (lane == 0) rdiag[j] = rd;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -186,17 +192,18 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
   const int idx = 4 * blockIdx.x + wave;
   if (idx >= n_rows) return;
   const long long i0 = (long long)panel_row(idx, k, g.nbt) * NB;
-  double* dst = Ao + (i0 + lane) * g.Na + k0;
+  double* dst = Ao + k0 * g.Na + i0 + lane;              // (i0 + lane, k0 + t) at dst[t Na]
   if (idx == 0) {
 #pragma unroll
     for (int t = 0; t < NB; ++t)
-      if (t <= lane) dst[t] = L[lane][t];
+      if (t <= lane) dst[t * g.Na] = L[lane][t];
     return;
   }
-  // x L_kk^T = a:  x_j = (a_j - sum_{t<j} x_t L_jt) / L_jj   (two partial sums for ILP)
+  // x L_kk^T = a:  x_j = (a_j - sum_{t<j} x_t L_jt) / L_jj   (two partial sums for ILP; the
+  // division as a product with the reciprocal the factorisation computed)
   double x[NB];
 #pragma unroll
-  for (int t = 0; t < NB; ++t) x[t] = dst[t];
+  for (int t = 0; t < NB; ++t) x[t] = dst[t * g.Na];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     double s0 = x[j], s1 = 0.0;
@@ -205,10 +212,10 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A,
       if (t & 1) s1 = __builtin_fma(-x[t], L[j][t], s1);
       else s0 = __builtin_fma(-x[t], L[j][t], s0);
     }
-    x[j] = (s0 + s1) / L[j][j];
+    x[j] = (s0 + s1) * rdiag[j];
   }
 #pragma unroll
-  for (int t = 0; t < NB; ++t) dst[t] = x[t];
+  for (int t = 0; t < NB; ++t) dst[t * g.Na] = x[t];
 }
 
 // ----------------------------------------------------------------------- update
@@ -227,8 +234,10 @@ __device__ __forceinline__ void tri_decode(long long t, int& i, int& j) {
 
 // Trailing update of step k: A_pq -= L_pk L_qk^T for every live tile, k < q <= p:
 //   T1 top x top (m (m + 1) / 2), T2 bottom x top (ra m), T3 bottom x bottom (ra (ra + 1) / 2),
-//   m = nbt - k - 1.  L_pk and L_qk are staged in LDS (row-major, stride 66); wave w computes
-//   rows 16 w .. 16 w + 15 of the tile as 4 MFMA blocks over 16 k-steps.
+//   m = nbt - k - 1.  L_pk and L_qk are staged in LDS transposed (PT[c][r], stride 66, from
+//   coalesced column-major loads); the MFMAs compute C^T = L_qk L_pk^T so that a lane's output
+//   rows are consecutive rows of the column-major A: wave w takes q-rows 16 w .. 16 w + 15 of
+//   the tile against 4 blocks of 16 p-rows, over 16 k-steps.
 __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, Aug g, int k, int ra) {
   extern __shared__ double lds[];
   double* P = lds;
@@ -257,9 +266,9 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   const long long k0 = (long long)k * NB, p0 = (long long)p * NB, q0 = (long long)q * NB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int e = tid; e < NB * NB; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    P[r * LS + c] = Ao[(p0 + r) * g.Na + k0 + c];
-    Q[r * LS + c] = Ao[(q0 + r) * g.Na + k0 + c];
+    const int r = e & 63, c = e >> 6;                     // (row r, column c) of the tiles
+    P[c * LS + r] = Ao[(k0 + c) * g.Na + p0 + r];
+    Q[c * LS + r] = Ao[(k0 + c) * g.Na + q0 + r];
   }
   __syncthreads();
   d4 acc[4];
@@ -268,16 +277,18 @@ __global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A
   const int arow = 16 * wave + (lane & 15), ca = lane >> 4;
 #pragma unroll
   for (int s = 0; s < NB / 4; ++s) {
-    const double av = P[arow * LS + 4 * s + ca];
+    const double av = Q[(4 * s + ca) * LS + arow];        // A = L_qk rows 16 w ..
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[b] = mfma64(av, Q[(16 * b + (lane & 15)) * LS + 4 * s + ca], acc[b]);
+    for (int b = 0; b < 4; ++b)                           // B = L_pk^T, p-rows 16 b ..
+      acc[b] = mfma64(av, P[(4 * s + ca) * LS + 16 * b + (lane & 15)], acc[b]);
   }
-  // D[(l >> 4) + 4 r][l & 15] of block (wave, b) -> row 16 wave + (l >> 4) + 4 r, col 16 b + (l & 15)
+  // D[(l >> 4) + 4 r][l & 15] of block (wave, b): q-row 16 wave + (l >> 4) + 4 r, p-row
+  // 16 b + (l & 15), i.e. element (p0 + p-row, q0 + q-row) of A, column-major
 #pragma unroll
   for (int b = 0; b < 4; ++b)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      double* c = Ao + (p0 + 16 * wave + (lane >> 4) + 4 * r) * g.Na + q0 + 16 * b + (lane & 15);
+      double* c = Ao + (q0 + 16 * wave + (lane >> 4) + 4 * r) * g.Na + p0 + 16 * b + (lane & 15);
       *c -= acc[b][r];
     }
 }
@@ -315,7 +326,7 @@ __global__ void inv_finish_kernel(double* __restrict__ out, const double* __rest
        t += (long long)gridDim.x * blockDim.x) {
     const long long i = t / n, j = t - i * n;
     const long long r = i >= j ? i : j, c = i >= j ? j : i;
-    out[(long long)o * n * n + t] = -Ao[(np_ + r) * g.Na + np_ + c];
+    out[(long long)o * n * n + t] = -Ao[(np_ + c) * g.Na + np_ + r];
   }
 }
 
