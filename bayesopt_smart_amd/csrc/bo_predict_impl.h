@@ -469,6 +469,12 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           const int n_here = upper ? (ch - e0 + 1 < eN ? ch - e0 + 1 : eN) : eN;
           auto ep_body = [&](auto e_c) {
             constexpr int e = decltype(e_c)::value;
+            // explicit / Sobol candidates: keep the workgroup's 4 waves on the same E-pair block
+            // (they stream identical W data, so 3 of 4 L2 requests become L1 hits).  W beyond
+            // an XCD's 4 MB L2 (C4: 12.6 MB, C5: 50 MB) otherwise comes from MALL once per
+            // wave: C5-f64 1124 -> 869 ms, C4 118.8 -> 116.8 ms (same box).  The SEP path is
+            // left unsynchronised (lockstep measured 4 % slower at C3, 7 % at C2: its W fits L2).
+            if constexpr (!SEP) __builtin_amdgcn_s_barrier();
             if constexpr (e == 0) {
               gen.s0(K, al, mu_on, chn, g, An);
               __builtin_amdgcn_sched_barrier(0);
