@@ -138,6 +138,117 @@ static __global__ __launch_bounds__(1024) void bo_argbest_merge_kernel(const Top
   }
 }
 
+// Per-candidate outputs (mu, var, UCB, acq, ...): written once, read by the next launch or the
+// host -- streaming stores, so that they do not evict the L2-resident W stream.
+__device__ __forceinline__ void bo_out_store(double* p, double v) { __builtin_nontemporal_store(v, p); }
+
+// Workgroup-wide best entry (selection order) of one entry per thread; every thread gets it.
+// `red` is a __shared__ scratch of blockDim.x / 64 entries.
+__device__ __forceinline__ TopEntry bo_block_best(double v, long long i, TopEntry* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) {
+    const double ov = __shfl_xor(v, m, 64);
+    const long long oi = __shfl_xor(i, m, 64);
+    if (bo_better(ov, oi, v, i)) { v = ov; i = oi; }
+  }
+  if (lane == 0) { red[wave].v = v; red[wave].i = i; }
+  __syncthreads();
+  TopEntry b = red[0];
+  for (int w = 1; w < nw; ++w)
+    if (bo_better(red[w].v, red[w].i, b.v, b.i)) b = red[w];
+  __syncthreads();
+  return b;
+}
+
+// Final merge of n_lists sorted top-q lists ([n_lists][q], any q <= BO_MAX_TOPQ) into out_v /
+// out_i in selection order; one workgroup of 1024 threads.
+//   T = the best of the lists' q-th entries.  The list holding T has q entries not worse than
+//   T, so the global top-q lies in S = {valid entries not worse than T} -- normally a handful
+//   (about q .. 2q).  S is compacted into LDS and each entry's rank in S (the number of S
+//   entries before it) is counted directly; rank r < q goes to slot r.  When |S| > 64 (mass
+//   ties, or fewer than q valid entries in total) q rounds of a workgroup arg-best over S, each
+//   retiring its winner by the strict order, finish instead.  Loads are batched 8 deep per
+//   thread.  (Round 1's q rounds of arg-best over every entry: 14 us at C2; an in-kernel
+//   last-workgroup merge measured slower still: its device-scope release fence and serial
+//   chain cost ~25 us at the end of the fused kernel.)
+static __global__ __launch_bounds__(1024) void bo_topq_merge_kernel(const TopEntry* __restrict__ L,
+                                                                    long long n_lists, int q,
+                                                                    double* __restrict__ out_v,
+                                                                    long long* __restrict__ out_i) {
+  __shared__ TopEntry s_red[16];
+  __shared__ TopEntry s_buf[64];
+  __shared__ int s_cnt;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) s_cnt = 0;
+  double bv = -__builtin_inf();
+  long long bi = -1;
+  for (long long l0 = tid; l0 < n_lists; l0 += 8 * nt) {
+    TopEntry e[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long l = l0 + (long long)u * nt;
+      e[u] = l < n_lists ? L[l * q + q - 1] : TopEntry{-__builtin_inf(), -1};
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (bo_better(e[u].v, e[u].i, bv, bi)) { bv = e[u].v; bi = e[u].i; }
+  }
+  const TopEntry T = bo_block_best(bv, bi, s_red);
+  const long long total = n_lists * q;
+  for (long long k0 = tid; k0 < total; k0 += 8 * nt) {
+    TopEntry e[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long k = k0 + (long long)u * nt;
+      e[u] = k < total ? L[k] : TopEntry{-__builtin_inf(), -1};
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (e[u].i >= 0 && !bo_better(T.v, T.i, e[u].v, e[u].i)) {
+        const int p = atomicAdd(&s_cnt, 1);
+        if (p < 64) s_buf[p] = e[u];
+      }
+    }
+  }
+  __syncthreads();
+  const int cnt = s_cnt;
+  if (cnt <= 64) {
+    if (tid < 64) {
+      if (tid < cnt) {
+        const TopEntry me = s_buf[tid];
+        int rank = 0;
+        for (int m = 0; m < cnt; ++m) rank += bo_better(s_buf[m].v, s_buf[m].i, me.v, me.i) ? 1 : 0;
+        if (rank < q) { out_v[rank] = me.v; out_i[rank] = me.i; }
+      } else if (tid < q) {
+        out_v[tid] = -__builtin_inf();
+        out_i[tid] = -1;
+      }
+    }
+    return;
+  }
+  double pv = 0.0;
+  long long pi = -1;                                 // previous winner (none yet)
+  for (int r = 0; r < q; ++r) {
+    double cv = -__builtin_inf();
+    long long ci = -1;
+    for (long long k = tid; k < total; k += nt) {
+      const TopEntry e = L[k];
+      if (e.i < 0 || bo_better(T.v, T.i, e.v, e.i)) continue;
+      if (pi >= 0 && !bo_better(pv, pi, e.v, e.i)) continue;   // already selected
+      if (bo_better(e.v, e.i, cv, ci)) { cv = e.v; ci = e.i; }
+    }
+    const TopEntry w = bo_block_best(cv, ci, s_red);
+    if (tid == 0) { out_v[r] = w.i >= 0 ? w.v : -__builtin_inf(); out_i[r] = w.i; }
+    pv = w.v;
+    pi = w.i;
+    if (w.i < 0) {
+      for (int t = r + 1 + tid; t < q; t += nt) { out_v[t] = -__builtin_inf(); out_i[t] = -1; }
+      break;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Sobol candidates (BO_CAND_SOBOL): direction numbers (host) and one coordinate (device).
 // ---------------------------------------------------------------------------------------

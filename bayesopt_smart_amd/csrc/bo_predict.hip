@@ -249,37 +249,6 @@ __device__ void pack_range(long long t0, long long stride, d2* __restrict__ out,
   }
 }
 
-// Merge the per-wave lists [n_lists][q] into the final top-q (one workgroup, 16 waves).
-__global__ __launch_bounds__(1024) void topq_merge_kernel(const TopEntry* __restrict__ lists,
-                                                          int n_lists, int q,
-                                                          double* __restrict__ out_v,
-                                                          long long* __restrict__ out_i) {
-  __shared__ TopEntry stage[16 * BO_MAX_TOPQ];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  double lv = -__builtin_inf();
-  long long li = -1;
-  const long long total = (long long)n_lists * q;
-  for (long long base = (long long)wave * 16; base < total; base += (long long)nw * 16) {
-    double nv = -__builtin_inf();
-    long long ni = -1;
-    if (lane < 16 && base + lane < total) { nv = lists[base + lane].v; ni = lists[base + lane].i; }
-    bo_wave_topq_insert(lv, li, nv, ni, q);
-  }
-  if (lane < q) { stage[wave * q + lane].v = lv; stage[wave * q + lane].i = li; }
-  __syncthreads();
-  if (wave == 0) {
-    double fv = -__builtin_inf();
-    long long fi = -1;
-    for (int base = 0; base < nw * q; base += 16) {
-      double nv = -__builtin_inf();
-      long long ni = -1;
-      if (lane < 16 && base + lane < nw * q) { nv = stage[base + lane].v; ni = stage[base + lane].i; }
-      bo_wave_topq_insert(fv, fi, nv, ni, q);
-    }
-    if (lane < q) { out_v[lane] = fv; out_i[lane] = fi; }
-  }
-}
-
 __global__ void selftest_mfma_kernel(const double* a, const double* b, double* d) {
   const int l = threadIdx.x;
   const double av = a[(l & 15) * 4 + (l >> 4)];  // A[i=l&15][k=l>>4]
@@ -440,7 +409,8 @@ __global__ void selftest_mfma32_kernel(const float* a, const float* b, float* d)
 inline int pad_rows(long long n) { return (int)((n + 31) / 32 * 32); }
 inline int pad_dim(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : (d <= 6 ? 6 : 8)); }
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-constexpr size_t kLdsDoubles = 160 * 1024 / sizeof(double);
+constexpr size_t kLdsBytes = 160 * 1024;
+constexpr size_t kLdsDoubles = kLdsBytes / sizeof(double);
 
 int num_cus() {
   static int cus = 0;
@@ -478,7 +448,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   if ((d->mode & BO_PREDICT_FP32) && !kmem) {
     const int n_pad = (int)((n + 63) / 64 * 64);
     const size_t lds = ((size_t)n_pad * pl->dim_pad + (size_t)d->n_obj * n_pad) * sizeof(float);
-    if (lds <= 160 * 1024) {
+    if (lds <= kLdsBytes) {
       pl->fp32 = true;
       pl->n_pad = n_pad;
       pl->ns = 16;
@@ -518,6 +488,10 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
       lds = bo::kExpTab;
     }
     pl->lds = lds * sizeof(double);
+    // N <= 128: the 4-accumulator kernel, two workgroups per CU (LDS permitting)
+#ifndef BO_ABL_NOSMALL
+    pl->small = !pl->grows && n_pad <= 4 * 32 && pl->lds <= kLdsBytes / 2 - 1024;
+#endif
   }
   if (kmem) {
     int n_pad = pad_rows(n);
@@ -543,7 +517,8 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   const long long n_tiles = (d->n_cand + kTile - 1) / kTile;
   pl->n_tiles = n_tiles;
   const int cus = query_device ? num_cus() : 256;
-  pl->grid = (int)(n_tiles < cus ? (n_tiles > 0 ? n_tiles : 1) : cus);
+  const int slots = pl->small ? 2 * cus : cus;
+  pl->grid = (int)(n_tiles < slots ? (n_tiles > 0 ? n_tiles : 1) : slots);
   pl->off_alpha = align256(w_bytes);
   pl->off_xpad = pl->off_alpha + align256((size_t)d->n_obj * n_pad * sizeof(double));
   pl->off_xc = pl->off_xpad + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
@@ -757,13 +732,8 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   if (e != hipSuccess) return BO_ERR_HIP;
   if (timed) timer_mark(s);
   if (d->topq > 0) {
-    const int n_lists = pl.grid * pl.waves;
-    if (d->topq <= 16 && (long long)n_lists * d->topq <= 8 * 1024)
-      hipLaunchKernelGGL(bo_argbest_merge_kernel, dim3(1), dim3(1024), 0, s, partial,
-                         (long long)n_lists * d->topq, d->topq, d->top_val, (long long*)d->top_idx);
-    else
-      hipLaunchKernelGGL(topq_merge_kernel, dim3(1), dim3(1024), 0, s, partial, n_lists,
-                         d->topq, d->top_val, (long long*)d->top_idx);
+    hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(1024), 0, s, partial,
+                       (long long)pl.grid * pl.waves, d->topq, d->top_val, (long long*)d->top_idx);
     BO_CHECK_HIP(hipGetLastError());
   }
   return BO_OK;

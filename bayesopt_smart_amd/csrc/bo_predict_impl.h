@@ -71,6 +71,7 @@ struct Plan {
   int off_tbl, off_rw;   // LDS offsets in doubles
   bool rw_cache;         // SEP row factors cached per objective
   bool fp32;             // cm32_predict_kernel (BO_PREDICT_FP32)
+  bool small;            // N <= 128: 4 E-pair accumulators, two workgroups per CU
   int off_exp;
   int grid, waves;       // persistent grid, waves per workgroup
   long long n_tiles;
@@ -261,12 +262,14 @@ struct KRows {
 // pairs of the chunk's first E-pair (sched barriers pin them), so that every LDS round trip
 // of the generation (SEP: row factor + table index, then the table value; the alpha values
 // of the mean) completes under MFMAs instead of stalling the wave before the chunk:
-//   s0: rv[f], rb[f], alpha[f] loads     s1: table loads T[rb - jl]     s2: the products.
+//   s0: rv[f], rb[f], alpha[f] loads     s1: table loads T[rb - jl] into Bn     s2: Bn *= rv.
 // The exp path (!SEP) is VALU work that serialises with f64 MFMAs anyway: all of it in s2.
+// The alpha values A of the next chunk are consumed (mu += A . Bn) right after s2, within the
+// same chunk, so that they need no second register set.
 template <int DIM, bool SEP>
 struct KGen {
   using KR = KRows<DIM, SEP>;
-  double rv[8], tv[8];
+  double rv[8];
   int rb[8];
   __device__ __forceinline__ void s0(const KR& K, const double* al, bool mu_on, int ch,
                                      int g, double (&A)[8]) {
@@ -289,16 +292,16 @@ struct KGen {
       }
     }
   }
-  __device__ __forceinline__ void s1(const KR& K) {
+  __device__ __forceinline__ void s1(const KR& K, double (&B)[8]) {
     if (SEP) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) tv[s] = K.tb[rb[s] - K.jl];
+      for (int s = 0; s < 8; ++s) B[s] = K.tb[rb[s] - K.jl];
     }
   }
   __device__ __forceinline__ void s2(const KR& K, int ch, int g, double (&B)[8]) {
     if (SEP) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) B[s] = rv[s] * tv[s];
+      for (int s = 0; s < 8; ++s) B[s] *= rv[s];
     } else {
       K.chunk(ch, g, B);
     }
@@ -329,7 +332,7 @@ struct KGen {
 // GROWS: the training rows, |x_f|^2 and alpha are read from global memory (L2-resident)
 // instead of LDS, for N whose rows do not fit the 160 KiB LDS (the reference has no N cap).
 // ---------------------------------------------------------------------------------------
-template <int DIM, bool SEP, bool UPPER, bool GROWS>
+template <int DIM, bool SEP, bool UPPER, bool GROWS, int MAXEP>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   constexpr bool upper = UPPER;
   // training rows (SEP: original grid coordinates; otherwise centred on z = row 0), alpha
@@ -438,27 +441,27 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       prime_ring(wr, voff, base, wa, wb);
       int pos = 0;
       double mpart = 0.0, qpart = 0.0;
-      d4 acc[kCMaxEp][2];
+      d4 acc[MAXEP][2];
       // E-pairs in groups of kCMaxEp (the accumulators one wave holds: 512 rows); a group
       // streams the chunks that touch it (c >= its first E-pair when upper, all otherwise) and
       // regenerates their K*.  One group when N <= 512.
-      for (int e0 = 0; e0 < nch; e0 += kCMaxEp) {
-        const int eN = nch - e0 < kCMaxEp ? nch - e0 : kCMaxEp;
+      for (int e0 = 0; e0 < nch; e0 += MAXEP) {
+        const int eN = nch - e0 < MAXEP ? nch - e0 : MAXEP;
         // all kCMaxEp accumulator pairs zeroed unconditionally (zeroing only the group's eN
         // pairs behind nested guards measured 1-2 % slower at C2/C3/C4)
 #pragma unroll
-        for (int e = 0; e < kCMaxEp; ++e) {
+        for (int e = 0; e < MAXEP; ++e) {
           acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
           acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
         }
-        // one chunk: MFMAs from register set B while the next chunk's K* (and its alpha
-        // values, An) is generated into Bn in three stages inside E-pair 0's MFMA stream (the
-        // sets alternate: no register copies between the chunks).  Branch-free: the last chunk
-        // regenerates itself (chn clamped) and groups after the first add 0 x alpha to mu.
-        const bool mu_on = e0 == 0;
+        // one chunk: MFMAs from register set B while the next chunk's K* is generated into Bn
+        // in three stages inside E-pair 0's MFMA stream (the sets alternate: no register
+        // copies between the chunks), then mu += alpha . Bn.  Branch-free: the last chunk
+        // regenerates itself (chn clamped; its alpha values zeroed) and groups after the first
+        // add 0 x alpha to mu.
         KGen<DIM, SEP> gen;
-        auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8], const double (&A)[8],
-                              double (&An)[8]) {
+        auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8]) {
+          double An[8];
           // next chunk: ascending (dense) / descending (upper); the last one regenerates itself
           const int chn = upper ? (ch > e0 ? ch - 1 : ch) : (ch + 1 < nch ? ch + 1 : ch);
           // the group's E-pairs touching chunk ch, ascending: the first n_here of them (e0 + e
@@ -476,7 +479,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             // left unsynchronised (lockstep measured 4 % slower at C3, 7 % at C2: its W fits L2).
             if constexpr (!SEP) __builtin_amdgcn_s_barrier();
             if constexpr (e == 0) {
-              gen.s0(K, al, mu_on, chn, g, An);
+              gen.s0(K, al, e0 == 0 && chn != ch, chn, g, An);
               __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
@@ -493,16 +496,16 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               if constexpr (e == 0) {
                 if (pp == 0) {
                   __builtin_amdgcn_sched_barrier(0);
-                  gen.s1(K);
-                  __builtin_amdgcn_sched_barrier(0);
-                } else if (pp == 1) {
-                  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                  for (int s = 0; s < 8; ++s) mpart = __builtin_fma(A[s], B[s], mpart);
+                  gen.s1(K, Bn);
                   __builtin_amdgcn_sched_barrier(0);
                 } else if (pp == 2) {
                   __builtin_amdgcn_sched_barrier(0);
                   gen.s2(K, chn, g, Bn);
+                  __builtin_amdgcn_sched_barrier(0);
+                } else if (pp == 3) {
+                  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                  for (int s = 0; s < 8; ++s) mpart = __builtin_fma(An[s], Bn[s], mpart);
                   __builtin_amdgcn_sched_barrier(0);
                 }
               }
@@ -521,26 +524,28 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               }
             }
           };
-          EpChain<0, kCMaxEp>::run(ep_body, n_here);
+          EpChain<0, MAXEP>::run(ep_body, n_here);
         };
         const int c0 = upper ? nch - 1 : 0;
-        double BX[8], BY[8], AX[8], AY[8];
+        double BX[8], BY[8];
         K.chunk(c0, g, BX);
+        if (e0 == 0) {
 #pragma unroll
-        for (int s = 0; s < 8; ++s) AX[s] = mu_on ? al[32 * c0 + 4 * s + g] : 0.0;
+          for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * c0 + 4 * s + g], BX[s], mpart);
+        }
         int ch = c0;
         if (upper) {
           for (; ch - 1 >= e0; ch -= 2) {
-            chunk_step(ch, BX, BY, AX, AY);
-            chunk_step(ch - 1, BY, BX, AY, AX);
+            chunk_step(ch, BX, BY);
+            chunk_step(ch - 1, BY, BX);
           }
-          if (ch >= e0) chunk_step(ch, BX, BY, AX, AY);
+          if (ch >= e0) chunk_step(ch, BX, BY);
         } else {
           for (; ch + 1 < nch; ch += 2) {
-            chunk_step(ch, BX, BY, AX, AY);
-            chunk_step(ch + 1, BY, BX, AY, AX);
+            chunk_step(ch, BX, BY);
+            chunk_step(ch + 1, BY, BX);
           }
-          if (ch < nch) chunk_step(ch, BX, BY, AX, AY);
+          if (ch < nch) chunk_step(ch, BX, BY);
         }
         // dense: q = k . z after the last chunk, chunk ep's K* regenerated.  Software-pipelined:
         // E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence and multiplied after
@@ -549,16 +554,16 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           KGen<DIM, SEP> gq[2];
           double S[2][8];
           gq[0].s0k(K, e0, g);
-          gq[0].s1(K);
+          gq[0].s1(K, S[0]);
           gq[0].s2(K, e0, g, S[0]);
 #pragma unroll
-          for (int e = 0; e < kCMaxEp; ++e) {
+          for (int e = 0; e < MAXEP; ++e) {
             if (e < eN) {
               const int cur = e & 1, nxt = cur ^ 1;
               const bool more = e + 1 < eN;
               if (more) gq[nxt].s0k(K, e0 + e + 1, g);
               mfma_fence<true, 64>(acc[e][0], acc[e][1]);
-              if (more) gq[nxt].s1(K);
+              if (more) gq[nxt].s1(K, S[nxt]);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 qpart = __builtin_fma(S[cur][r], acc[e][0][r], qpart);
@@ -583,14 +588,14 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       acq = (o == 0) ? u : acq + u;                                    // acquisition.py:108
       if (valid && g == 0) {
         const long long off = (long long)o * a.ld_out + j;
-        if (a.mu) a.mu[off] = mu;
-        if (a.var) a.var[off] = var;
-        if (a.std_mu) a.std_mu[off] = smu;
-        if (a.std_var) a.std_var[off] = svar;
-        if (a.ucb) a.ucb[off] = u;
+        if (a.mu) bo_out_store(a.mu + off, mu);
+        if (a.var) bo_out_store(a.var + off, var);
+        if (a.std_mu) bo_out_store(a.std_mu + off, smu);
+        if (a.std_var) bo_out_store(a.std_var + off, svar);
+        if (a.ucb) bo_out_store(a.ucb + off, u);
       }
     }
-    if (valid && g == 0 && a.acq) a.acq[j] = acq;
+    if (valid && g == 0 && a.acq) bo_out_store(a.acq + j, acq);
     if (a.topq > 0) {
       // exclusion of evaluated points (acquisition.py:137-139: all coordinates equal)
       bool hit = false;
@@ -636,18 +641,25 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
     }
   }
   BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
-  if (a.topq > 0 && lane < a.topq) {
-    TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
-    dst[lane].v = top_v;
-    dst[lane].i = top_i;
+  if (a.topq > 0) {
+    if (lane < a.topq) {
+      TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
+      dst[lane].v = top_v;
+      dst[lane].i = top_i;
+    }
   }
 }
 
 // GRID: the host found the grid structure usable (rows of 16); the device flag then says
 // whether every training point lies on the grid's last axis (sep_check in the prep kernel).
 // GROWS: training rows / alpha stay in global memory (N beyond the LDS budget).
-template <int DIM, bool GRID, bool UPPER, bool GROWS>
-__global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
+// MAXEP: E-pair accumulators per wave.  16 (256 AGPRs, one wave per SIMD) in general; 4 for
+// N <= 128 (one group), with two workgroups per CU: at such N the per-tile serial sections
+// (W ring priming, first-chunk generation, accumulator fences, the epilogue's divisions and
+// square roots, the top-q shuffles) are long against the tile's 160 MFMAs, and the second
+// wave on each SIMD issues its MFMAs while the first waits in them.
+template <int DIM, bool GRID, bool UPPER, bool GROWS, int MAXEP>
+__global__ __launch_bounds__(256, MAXEP <= 4 ? 2 : 1) void cm_predict_kernel(const FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x;
   const bool sep = !GROWS && GRID && __builtin_amdgcn_readfirstlane(*a.sep_flag) == 0;
@@ -671,14 +683,14 @@ __global__ __launch_bounds__(256, 1) void cm_predict_kernel(const FusedArgs a) {
   }
   __syncthreads();
   if constexpr (GRID && !GROWS) {
-    if (sep) { cm_tiles<DIM, true, UPPER, false>(a, smem); return; }
+    if (sep) { cm_tiles<DIM, true, UPPER, false, MAXEP>(a, smem); return; }
   }
-  cm_tiles<DIM, false, UPPER, GROWS>(a, smem);
+  cm_tiles<DIM, false, UPPER, GROWS, MAXEP>(a, smem);
 }
 
-template <int DIM, bool GRID, bool UPPER, bool GROWS>
+template <int DIM, bool GRID, bool UPPER, bool GROWS, int MAXEP>
 hipError_t launch_cm_k(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) {
-  auto k = cm_predict_kernel<DIM, GRID, UPPER, GROWS>;
+  auto k = cm_predict_kernel<DIM, GRID, UPPER, GROWS, MAXEP>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
@@ -690,9 +702,12 @@ hipError_t launch_cm_k(const FusedArgs& fa, int grid, size_t lds, hipStream_t st
 
 template <int DIM, bool UPPER, bool GROWS>
 hipError_t launch_cm_u(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
-  if constexpr (GROWS) return launch_cm_k<DIM, false, UPPER, true>(fa, pl.grid, pl.lds, st);
-  return pl.sep ? launch_cm_k<DIM, true, UPPER, false>(fa, pl.grid, pl.lds, st)
-                : launch_cm_k<DIM, false, UPPER, false>(fa, pl.grid, pl.lds, st);
+  if constexpr (GROWS) return launch_cm_k<DIM, false, UPPER, true, bo::kCMaxEp>(fa, pl.grid, pl.lds, st);
+  if (pl.small)
+    return pl.sep ? launch_cm_k<DIM, true, UPPER, false, 4>(fa, pl.grid, pl.lds, st)
+                  : launch_cm_k<DIM, false, UPPER, false, 4>(fa, pl.grid, pl.lds, st);
+  return pl.sep ? launch_cm_k<DIM, true, UPPER, false, bo::kCMaxEp>(fa, pl.grid, pl.lds, st)
+                : launch_cm_k<DIM, false, UPPER, false, bo::kCMaxEp>(fa, pl.grid, pl.lds, st);
 }
 
 template <int DIM>
@@ -866,14 +881,14 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
       acq = (o == 0) ? u : acq + u;                                       // acquisition.py:108
       if (valid && g == 0) {
         const long long off = (long long)o * a.ld_out + j;
-        if (a.mu) a.mu[off] = mu;
-        if (a.var) a.var[off] = var;
-        if (a.std_mu) a.std_mu[off] = smu;
-        if (a.std_var) a.std_var[off] = svar;
-        if (a.ucb) a.ucb[off] = u;
+        if (a.mu) bo_out_store(a.mu + off, mu);
+        if (a.var) bo_out_store(a.var + off, var);
+        if (a.std_mu) bo_out_store(a.std_mu + off, smu);
+        if (a.std_var) bo_out_store(a.std_var + off, svar);
+        if (a.ucb) bo_out_store(a.ucb + off, u);
       }
     }
-    if (valid && g == 0 && a.acq) a.acq[j] = acq;
+    if (valid && g == 0 && a.acq) bo_out_store(a.acq + j, acq);
     if (a.topq > 0) {
       long long gi = valid ? a.cand_offset + j : -1;
       const double tv = __shfl(top_v, a.topq - 1, 64);
@@ -896,10 +911,12 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
     }
   }
   BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
-  if (a.topq > 0 && lane < a.topq) {
-    TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
-    dst[lane].v = top_v;
-    dst[lane].i = top_i;
+  if (a.topq > 0) {
+    if (lane < a.topq) {
+      TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
+      dst[lane].v = top_v;
+      dst[lane].i = top_i;
+    }
   }
 }
 

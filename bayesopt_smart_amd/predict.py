@@ -170,7 +170,7 @@ MODES = {"auto": 0, "dense": 1, "auto-exp": 2, "dense-exp": 3, "fp32": 4}
 def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, prior_variance,
                     length_scales, betas, *, outputs=("mu", "var", "acq"), topq=0,
                     excl_points=None, offset=0, count=None, out=None, device=None, mode="auto",
-                    top_rec=None):
+                    top_rec=None, prepare=False):
     """Score candidates [offset, offset+count) of `cands`.
 
     x_train [N, d], y_train [N or T, n_obj] (only the first N rows are read), kinv
@@ -188,6 +188,9 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     ``top_rec`` (optional f64 device tensor [2 topq]): the selection is written into it as one
     16-B-per-entry record block -- values in [:topq], int64 indices (bit pattern) in [topq:] --
     so that the multi-GPU exchange is ONE all_gather of it (distributed.exchange_topq_rec).
+
+    ``prepare=True`` returns a PreparedPredict instead of launching: calling it launches this
+    call again (same buffers), without re-validating.
     """
     dev = require_device(device)
     x_train = as_dev(x_train, dev)
@@ -245,10 +248,26 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     if nbytes == 0:
         raise _lib.BoNativeError(_lib.ERR_ARG, "bo_predict_workspace_size")
     ws = Workspace.get(nbytes, dev)
-    _lib.check(lib.bo_predict_acquire(desc, ws.data_ptr(), ws.numel(), stream_handle(dev)),
-               "bo_predict_acquire")
     res["_keepalive"] = (x_train, y_train, kinv, excl_points)
-    return res
+    call = PreparedPredict(lib, desc, ws, stream_handle(dev), res)
+    return call if prepare else call()
+
+
+class PreparedPredict:
+    """One validated bo_predict_acquire call (predict_acquire(..., prepare=True)): calling it
+    re-launches the whole chain -- preparation (W packing, alpha, rows), the fused kernel and its
+    in-kernel top-q merge -- on the same device buffers, which the caller may refill in place
+    between calls.  Like a library plan object, it skips only the host-side validation and the
+    descriptor build of predict_acquire (tens of microseconds of Python per call)."""
+
+    def __init__(self, lib, desc, ws, stream, res):
+        self._lib, self._desc, self._ws, self._stream, self.res = lib, desc, ws, stream, res
+        self._ws_ptr, self._ws_n = ws.data_ptr(), ws.numel()
+
+    def __call__(self):
+        _lib.check(self._lib.bo_predict_acquire(self._desc, self._ws_ptr, self._ws_n, self._stream),
+                   "bo_predict_acquire")
+        return self.res
 
 
 def merge_topq(vals, idxs, q):

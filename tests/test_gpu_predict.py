@@ -152,6 +152,31 @@ def test_edge_cases(bo):
     assert sorted(got[:2].tolist()) == [0, 1] and (got[2:] == -1).all()
 
 
+@pytest.mark.parametrize("m,q", [(300, 48), (None, 48), (None, 3), (70, 20)])
+def test_topq_merge_exact_order(bo, m, q):
+    """The final merge of the per-wave lists (bo_topq_merge_kernel): both its paths -- the
+    threshold set sorted by rank, and the arg-best rounds when that set exceeds 64 entries (here:
+    every wave holds fewer than q candidates) -- give exactly the selection order of the
+    acquisition array the same call wrote (NaN first, descending, ties by index)."""
+    import torch
+    d = predict_fixture("g1_predict_2d")
+    cand = d["cand"][:m]
+    m = len(cand)
+    cands = bo.predict.CandidateSet.explicit(cand)
+    r = bo.predict.predict_acquire(d["x"], d["y"], d["Kinv"], cands, d["pm"], d["pv"], d["ls"], d["betas"],
+                                   outputs=("acq",), topq=q)
+    torch.cuda.synchronize()
+    acq = r["acq"].cpu().numpy()
+    excl = _excluded(cand, d["x"])
+    a = np.where(excl, -np.inf, acq)
+    order = np.lexsort((np.arange(m), -a))
+    want = order[: min(q, int((~excl).sum()))]
+    got = r["top_idx"].cpu().numpy()
+    np.testing.assert_array_equal(got[: want.size], want)
+    assert (got[want.size:] == -1).all()
+    np.testing.assert_array_equal(r["top_val"].cpu().numpy()[: want.size], acq[want])
+
+
 def test_full_size_c3_properties(bo):
     """C3 at full size (N=512, M=1024^2 implicit grid): every candidate against the CPU
     reference (oracle/cpu_ref.c), top-q judged on the CPU acquisition array, deterministic
