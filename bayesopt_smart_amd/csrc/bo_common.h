@@ -79,6 +79,73 @@ __device__ __forceinline__ void bo_wave_topq_insert(double& lv, long long& li, d
   if (lane >= q) { lv = -__builtin_inf(); li = -1; }
 }
 
+__device__ __forceinline__ double bo_readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ long long bo_readlane_i(long long v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)v, l);
+  const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+  return ((long long)hi << 32) | (unsigned int)lo;
+}
+
+// The wave's running list: its q-th entry (the admission threshold), wave-uniform.
+__device__ __forceinline__ void bo_wave_topq_threshold(double lv, long long li, int q,
+                                                       double& tv, long long& ti) {
+  tv = bo_readlane_d(lv, q - 1);
+  ti = bo_readlane_i(li, q - 1);
+}
+
+// Merge the 16 candidates of a fused-kernel tile into the wave's running top-q list, q <= 16.
+// The list is in lanes 0..q-1 (sorted; lanes >= q empty); the candidates are (nv, ni) of lane
+// group 1 (lanes 16..31; every lane group holds the same 16).  Only the candidates beating the
+// list's q-th entry (N') take part: each element of list + N' counts the elements before it in
+// selection order (its final rank: list entries know their own position; the N' entries and the
+// list entries are broadcast by v_readlane, |N'| + q rounds), and the ranks < q are scattered
+// to their lanes by ds_permute.  Round 1 re-sorted all 64 lanes with a bitonic network (21
+// shuffle stages) whenever a candidate entered -- on spatially coherent acquisition surfaces
+// (a wave walking up a grid row) nearly every tile, ~6 us per tile at C2.
+__device__ __forceinline__ void bo_wave_topq_insert16(double& lv, long long& li, double nv,
+                                                      long long ni, int q) {
+  const int lane = threadIdx.x & 63;
+  double tv;
+  long long ti;
+  bo_wave_topq_threshold(lv, li, q, tv, ti);
+  const bool beat = (lane >> 4) == 1 && bo_better(nv, ni, tv, ti);
+  const unsigned long long nb = __ballot(beat);
+  if (nb == 0ull) return;
+  const bool isL = lane < q;
+  const double mv = isL ? lv : nv;
+  const long long mi = isL ? li : ni;
+  int rank = isL ? lane : 0;
+  for (unsigned long long m = nb; m; m &= m - 1) {
+    const int s = __builtin_ctzll(m);
+    rank += bo_better(bo_readlane_d(nv, s), bo_readlane_i(ni, s), mv, mi) ? 1 : 0;
+  }
+  for (int l = 0; l < q; ++l) {
+    const bool b = bo_better(bo_readlane_d(lv, l), bo_readlane_i(li, l), mv, mi);
+    rank += (beat && b) ? 1 : 0;
+  }
+  const bool keep = (isL || beat) && rank < q;
+  // targets: kept elements -> lane rank (< q <= 16); the others -> a lane >= 16 (the list
+  // lanes' own slot + 48, or their own lane), never one of 0..q-1
+  const int dst = keep ? rank : (lane < 16 ? lane + 48 : lane);
+  const long long vb = __double_as_longlong(mv);
+  const int v0 = __builtin_amdgcn_ds_permute(dst << 2, (int)vb);
+  const int v1 = __builtin_amdgcn_ds_permute(dst << 2, (int)(vb >> 32));
+  const int i0 = __builtin_amdgcn_ds_permute(dst << 2, (int)mi);
+  const int i1 = __builtin_amdgcn_ds_permute(dst << 2, (int)(mi >> 32));
+  if (lane < q) {
+    lv = __longlong_as_double(((long long)v1 << 32) | (unsigned int)v0);
+    li = ((long long)i1 << 32) | (unsigned int)i0;
+  } else {
+    lv = -__builtin_inf();
+    li = -1;
+  }
+}
+
 // Final merge of per-wave / per-workgroup top lists (`total` entries, <= 8 per thread of the
 // single 1024-thread workgroup, i.e. <= 8192): q rounds of a workgroup-wide arg-best over the
 // entries held in registers, the winner retired by its (unique) global index.  Used for q <= 16

@@ -449,11 +449,13 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         const int eN = nch - e0 < MAXEP ? nch - e0 : MAXEP;
         // all kCMaxEp accumulator pairs zeroed unconditionally (zeroing only the group's eN
         // pairs behind nested guards measured 1-2 % slower at C2/C3/C4)
+#ifndef BO_ABL_NOZERO
 #pragma unroll
         for (int e = 0; e < MAXEP; ++e) {
           acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
           acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
         }
+#endif
         // one chunk: MFMAs from register set B while the next chunk's K* is generated into Bn
         // in three stages inside E-pair 0's MFMA stream (the sets alternate: no register
         // copies between the chunks), then mu += alpha . Bn.  Branch-free: the last chunk
@@ -513,7 +515,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             // upper: E-pair e0 + e is complete after its own chunk (chunks descend), the last
             // body of that chunk: q += K*[chunk rows] . acc with the rows still in B (rows
             // 32 ep + g + 4r (+16) = B slots r (4 + r)); no regeneration
+#ifdef BO_ABL_NOQ
+            if constexpr (false) {
+#else
             if constexpr (UPPER) {
+#endif
               if (ch - e0 == e) {
                 mfma_fence<true, 64>(acc[e][0], acc[e][1]);
 #pragma unroll
@@ -582,9 +588,13 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       const double pv = a.pv[o], pm = a.pm[o];
       const double mu = pm + mpart;                                   // :486-488
       const double var = fmax(pv - qpart, BO_MIN_VARIANCE);           // :532-535
+#ifdef BO_ABL_NOEPI
+      const double smu = mu - pm, svar = var, u = smu + a.beta[o] * svar;
+#else
       const double smu = (mu - pm) / a.rsq_pv[o];                      // :563-565
       const double svar = var / pv;                                    // :568-570
       const double u = smu + a.beta[o] * sqrt(fabs(svar));             // acquisition.py:52
+#endif
       acq = (o == 0) ? u : acq + u;                                    // acquisition.py:108
       if (valid && g == 0) {
         const long long off = (long long)o * a.ld_out + j;
@@ -596,30 +606,35 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       }
     }
     if (valid && g == 0 && a.acq) bo_out_store(a.acq + j, acq);
+#ifdef BO_ABL_NOTOPQ
+    if (false) {
+#else
     if (a.topq > 0) {
-      // exclusion of evaluated points (acquisition.py:137-139: all coordinates equal)
+#endif
+      // exclusion of evaluated points (acquisition.py:137-139: all coordinates equal), tested
+      // only when a candidate would enter the wave's list
+      const long long gi0 = valid ? a.cand_offset + j : -1;
+      double tv;
+      long long ti;
+      bo_wave_topq_threshold(top_v, top_i, a.topq, tv, ti);
+      const bool need = gi0 >= 0 && bo_better(acq, gi0, tv, ti);
       bool hit = false;
-      if (SEP && !a.excl) {
-        // training points on this grid row whose last coordinate falls in the wave's 16
-        // columns; OR over the wave, bit jl is this lane's candidate
-        unsigned int xmask = 0;
-        for (int f = lane; f < a.n_train; f += 64) {
-          const int dx = rb[f] - (a.sep_S - 1) - col0;
-          if (on[f] && dx >= 0 && dx < 16) xmask |= 1u << dx;
-        }
-        unsigned int m = xmask;
+      if (__ballot(need) != 0ull) {
+        if (SEP && !a.excl) {
+          // training points on this grid row whose last coordinate falls in the wave's 16
+          // columns; OR over the wave, bit jl is this lane's candidate
+          unsigned int xmask = 0;
+          for (int f = lane; f < a.n_train; f += 64) {
+            const int dx = rb[f] - (a.sep_S - 1) - col0;
+            if (on[f] && dx >= 0 && dx < 16) xmask |= 1u << dx;
+          }
+          unsigned int m = xmask;
 #pragma unroll
-        for (int sh = 32; sh > 0; sh >>= 1) m |= (unsigned int)__shfl_xor((int)m, sh, 64);
-        hit = (m >> jl) & 1u;
-      } else {
-        // only candidates that would enter the wave's top-q are compared, exactly, in their
-        // original coordinates against the evaluated points in global memory; lane group g
-        // checks points g, g + 4, ...
-        const long long gi0 = valid ? a.cand_offset + j : -1;
-        const double tv = __shfl(top_v, a.topq - 1, 64);
-        const long long ti = __shfl(top_i, a.topq - 1, 64);
-        const bool need = gi0 >= 0 && bo_better(acq, gi0, tv, ti);
-        if (__ballot(need) != 0ull) {
+          for (int sh = 32; sh > 0; sh >>= 1) m |= (unsigned int)__shfl_xor((int)m, sh, 64);
+          hit = (m >> jl) & 1u;
+        } else {
+          // compared exactly, in the original coordinates, against the evaluated points in
+          // global memory; lane group g checks points g, g + 4, ...
           double co[DIM];
           load_candidate<DIM>(a, j, valid, co);
           const double* es = a.excl ? a.excl : a.xpad;
@@ -636,8 +651,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       const unsigned long long hb = __ballot(hit);
       const bool excluded =
           ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
-      const long long gi = (valid && !excluded) ? a.cand_offset + j : -1;
-      bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+      const long long gi = excluded ? -1 : gi0;
+      if (a.topq <= 16) bo_wave_topq_insert16(top_v, top_i, acq, gi, a.topq);
+      else bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
     }
   }
   BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
@@ -891,8 +907,9 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
     if (valid && g == 0 && a.acq) bo_out_store(a.acq + j, acq);
     if (a.topq > 0) {
       long long gi = valid ? a.cand_offset + j : -1;
-      const double tv = __shfl(top_v, a.topq - 1, 64);
-      const long long ti = __shfl(top_i, a.topq - 1, 64);
+      double tv;
+      long long ti;
+      bo_wave_topq_threshold(top_v, top_i, a.topq, tv, ti);
       const bool need = gi >= 0 && bo_better(acq, gi, tv, ti);
       if (__ballot(need) != 0ull) {
         // acquisition.py:137-139, exact f64 coordinates; lane group g checks points g, g+4, ...
@@ -907,7 +924,8 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
         const unsigned long long hb = __ballot(hit);
         if (((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull) gi = -1;
       }
-      bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+      if (a.topq <= 16) bo_wave_topq_insert16(top_v, top_i, acq, gi, a.topq);
+      else bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
     }
   }
   BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
