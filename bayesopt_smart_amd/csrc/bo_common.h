@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../../include/bo_amd.h"
 
@@ -146,63 +147,54 @@ __device__ __forceinline__ void bo_wave_topq_insert16(double& lv, long long& li,
   }
 }
 
-// Final merge of per-wave / per-workgroup top lists (`total` entries, <= 8 per thread of the
-// single 1024-thread workgroup, i.e. <= 8192): q rounds of a workgroup-wide arg-best over the
-// entries held in registers, the winner retired by its (unique) global index.  Used for q <= 16
-// by bo_predict_acquire and bo_select_topq (the bitonic merge serves larger q).
-static __global__ __launch_bounds__(1024) void bo_argbest_merge_kernel(const TopEntry* __restrict__ lists,
-                                                                       long long total, int q,
-                                                                       double* __restrict__ out_v,
-                                                                       long long* __restrict__ out_i) {
-  __shared__ TopEntry wbest[16];
-  __shared__ TopEntry win;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  double v[8];
-  long long ix[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const long long at = tid + (long long)k * blockDim.x;
-    v[k] = -__builtin_inf();
-    ix[k] = -1;
-    if (at < total) { v[k] = lists[at].v; ix[k] = lists[at].i; }
+// Hash key of a point for the exclusion of evaluated points (acquisition.py:137-139, exact
+// equality of every coordinate): -0.0 == 0.0, so the sign of zero is dropped; a point with a NaN
+// coordinate equals nothing (key 0 = "no key", never stored).  Keys are odd (0 marks empty
+// slots of the open-addressing tables).
+__host__ __device__ inline unsigned long long bo_point_key(const double* c, int dim) {
+  unsigned long long h = 0x9E3779B97F4A7C15ull;
+  for (int k = 0; k < dim; ++k) {
+    if (c[k] != c[k]) return 0ull;
+    const double z = c[k] == 0.0 ? 0.0 : c[k];
+    unsigned long long b;
+    memcpy(&b, &z, 8);
+    b ^= h + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    b ^= b >> 31; b *= 0x7FB5D329728EA185ull; b ^= b >> 27; b *= 0x81DADEF4BC2DD44Dull; b ^= b >> 33;
+    h = b;
   }
-  for (int r = 0; r < q; ++r) {
-    double bv = -__builtin_inf();
-    long long bi = -1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (bo_better(v[k], ix[k], bv, bi)) { bv = v[k]; bi = ix[k]; }
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) {
-      const double ov = __shfl_xor(bv, m, 64);
-      const long long oi = __shfl_xor(bi, m, 64);
-      if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  return h | 1ull;
+}
+
+// Insert point `e` (key != 0) into an open-addressing table of mask + 1 slots.
+__device__ __forceinline__ void bo_hash_insert(unsigned long long* keys, int* idx, unsigned int mask,
+                                               unsigned long long key, int e) {
+  for (unsigned int t = (unsigned int)key & mask;; t = (t + 1) & mask)
+    if (atomicCAS(keys + t, 0ull, key) == 0ull) { idx[t] = e; return; }
+}
+
+// Is point c (dim coordinates) one of the rows of pts ([*][ld]) stored in the table?
+__device__ __forceinline__ bool bo_hash_contains(const unsigned long long* keys, const int* idx,
+                                                 unsigned int mask, const double* pts, int ld,
+                                                 const double* c, int dim) {
+  const unsigned long long key = bo_point_key(c, dim);
+  if (key == 0ull) return false;
+  for (unsigned int t = (unsigned int)key & mask;; t = (t + 1) & mask) {
+    const unsigned long long kt = keys[t];
+    if (kt == 0ull) return false;
+    if (kt == key) {
+      const double* r = pts + (long long)idx[t] * ld;
+      bool eq = true;
+      for (int k = 0; k < dim; ++k) eq = eq && (r[k] == c[k]);
+      if (eq) return true;
     }
-    if (lane == 0) { wbest[wave].v = bv; wbest[wave].i = bi; }
-    __syncthreads();
-    if (wave == 0) {
-      bv = lane < nw ? wbest[lane].v : -__builtin_inf();
-      bi = lane < nw ? wbest[lane].i : -1;
-#pragma unroll
-      for (int m = 32; m > 0; m >>= 1) {
-        const double ov = __shfl_xor(bv, m, 64);
-        const long long oi = __shfl_xor(bi, m, 64);
-        if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-      }
-      if (lane == 0) {
-        win.v = bv;
-        win.i = bi;
-        out_v[r] = bv;
-        out_i[r] = bi;
-      }
-    }
-    __syncthreads();
-    const long long wi = win.i;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (wi >= 0 && ix[k] == wi) { v[k] = -__builtin_inf(); ix[k] = -1; }
-    __syncthreads();
   }
+}
+
+// table slots for n points: a power of two >= 2 n (load <= 1/2), at least 64
+inline unsigned int bo_hash_slots(long long n) {
+  unsigned int s = 64;
+  while (s < 2ull * (unsigned long long)(n > 0 ? n : 0)) s <<= 1;
+  return s;
 }
 
 // Per-candidate outputs (mu, var, UCB, acq, ...): written once, read by the next launch or the

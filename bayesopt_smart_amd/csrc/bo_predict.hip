@@ -344,6 +344,12 @@ struct PrepArgs {
   double* excl;
   const double* excl_in;
   int n_excl;
+  // hash set of the exclusion rows (the evaluated points, or the training rows when none are
+  // given): zeroed, then filled, by the rows block
+  unsigned long long* hkeys;
+  int* hidx;
+  unsigned int hslots;
+  int n_hash;                            // rows to insert (0: no table)
 };
 
 __global__ __launch_bounds__(256) void predict_prep_kernel(const PrepArgs p) {
@@ -393,6 +399,18 @@ __global__ __launch_bounds__(256) void predict_prep_kernel(const PrepArgs p) {
   for (int t = tid; t < p.n_excl * p.DIM; t += 256) {
     const int r = t / p.DIM, k = t - r * p.DIM;
     p.excl[t] = k < p.dim ? p.excl_in[(long long)r * p.dim + k] : 0.0;
+  }
+  if (p.n_hash > 0) {
+    for (unsigned int t = tid; t < p.hslots; t += 256) p.hkeys[t] = 0ull;
+    __syncthreads();
+    // keys over the DIM-padded coordinates (zeros past dim), read from the inputs
+    const double* src = p.excl_in ? p.excl_in : p.x;
+    for (int e = tid; e < p.n_hash; e += 256) {
+      double c[BO_MAX_DIM];
+      for (int k = 0; k < p.DIM; ++k) c[k] = k < p.dim ? src[(long long)e * p.dim + k] : 0.0;
+      const unsigned long long key = bo_point_key(c, p.DIM);
+      if (key != 0ull) bo_hash_insert(p.hkeys, p.hidx, p.hslots - 1, key, e);
+    }
   }
 }
 
@@ -523,7 +541,9 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   pl->off_xpad = pl->off_alpha + align256((size_t)d->n_obj * n_pad * sizeof(double));
   pl->off_xc = pl->off_xpad + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
   pl->off_excl = pl->off_xc + align256((size_t)n_pad * pl->dim_pad * sizeof(double));
-  pl->off_partial = pl->off_excl + align256((size_t)(pl->n_excl + 1) * pl->dim_pad * sizeof(double));
+  pl->off_hash = pl->off_excl + align256((size_t)(pl->n_excl + 1) * pl->dim_pad * sizeof(double));
+  pl->hash_slots = bo_hash_slots(pl->n_excl);
+  pl->off_partial = pl->off_hash + align256((size_t)pl->hash_slots * 12);
   // partial lists sized for the largest persistent grid any device could use
   pl->off_status = pl->off_partial +
                    align256((size_t)1024 * kWaves * (d->topq > 0 ? d->topq : 1) * sizeof(TopEntry));
@@ -636,6 +656,9 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.xpad = xpad;
   fa.xc = xc;
   fa.excl = d->excl_points ? excl : nullptr;
+  fa.hkeys = (const unsigned long long*)(ws + pl.off_hash);
+  fa.hidx = (const int*)(ws + pl.off_hash + (size_t)pl.hash_slots * 8);
+  fa.hmask = pl.hash_slots - 1;
   fa.wpack = wpack;
   fa.upper = (pl.cm && !(d->mode & BO_PREDICT_DENSE)) ? 1 : 0;
   fa.wpack_bytes = (unsigned int)((size_t)d->n_obj * pl.n_pad * pl.n_pad * sizeof(double));
@@ -703,6 +726,10 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     pa.excl = excl;
     pa.excl_in = d->excl_points;
     pa.n_excl = (kmem || !d->excl_points) ? 0 : pl.n_excl;
+    pa.hkeys = (unsigned long long*)fa.hkeys;
+    pa.hidx = (int*)fa.hidx;
+    pa.hslots = pl.hash_slots;
+    pa.n_hash = (kmem || d->topq == 0) ? 0 : pl.n_excl;
     hipLaunchKernelGGL(predict_prep_kernel, dim3((unsigned)(pa.pack_blocks + pa.alpha_blocks + 1)), dim3(256),
                        0, s, pa);
     BO_CHECK_HIP(hipGetLastError());

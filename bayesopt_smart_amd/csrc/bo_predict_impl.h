@@ -58,13 +58,17 @@ struct FusedArgs {
   int rw_cache;                          // SEP row factors kept for every objective (LDS permitting)
   int off_exp;                           // LDS offset (doubles) of the 2^(j/256) table
   SobolArgs sob;                         // kind BO_CAND_SOBOL: direction numbers, lo, scale
+  const unsigned long long* hkeys;       // hash set of the exclusion rows (excl or xpad), built
+  const int* hidx;                       // by the prep launch (bo_point_key over DIM coordinates)
+  unsigned int hmask;
 };
 
 // Host-side plan of one bo_predict_acquire call (bo_predict.hip: make_plan).
 struct Plan {
   int n_pad, ns, n_panels, dim_pad, n_excl;
   bool multi;
-  size_t off_alpha, off_xpad, off_xc, off_excl, off_partial, off_status, total;
+  size_t off_alpha, off_xpad, off_xc, off_excl, off_hash, off_partial, off_status, total;
+  unsigned int hash_slots;
   bool cm;               // chunk-major kernel (cm_predict_kernel)
   bool sep;              // ... with the integer-grid K* generation
   bool grows;            // ... training rows / alpha read from global memory (N beyond LDS)
@@ -633,19 +637,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           for (int sh = 32; sh > 0; sh >>= 1) m |= (unsigned int)__shfl_xor((int)m, sh, 64);
           hit = (m >> jl) & 1u;
         } else {
-          // compared exactly, in the original coordinates, against the evaluated points in
-          // global memory; lane group g checks points g, g + 4, ...
+          // compared exactly, in the original coordinates, with the evaluated points of the
+          // same hash (the prep launch's table; global memory)
           double co[DIM];
           load_candidate<DIM>(a, j, valid, co);
-          const double* es = a.excl ? a.excl : a.xpad;
-          const int ne = a.excl ? a.n_excl : a.n_train;
-          for (int e = g; e < ne; e += 4) {
-            const double* r = es + (size_t)e * DIM;
-            bool eq = true;
-#pragma unroll
-            for (int k = 0; k < DIM; ++k) eq = eq && (r[k] == co[k]);
-            hit = hit || eq;
-          }
+          hit = valid && bo_hash_contains(a.hkeys, a.hidx, a.hmask, a.excl ? a.excl : a.xpad, DIM, co, DIM);
         }
       }
       const unsigned long long hb = __ballot(hit);
@@ -795,7 +791,6 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
       __builtin_amdgcn_make_buffer_rsrc((void*)a.wpack, (short)0, (int)a.wpack_bytes, 0x00020000);
   const int voff = lane * 16;
   const double* es = a.excl ? a.excl : a.xpad;               // f64 [*][DIM] (exact equality)
-  const int ne = a.excl ? a.n_excl : a.n_train;
   double top_v = -__builtin_inf();
   long long top_i = -1;
   for (long long tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
@@ -912,15 +907,8 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
       bo_wave_topq_threshold(top_v, top_i, a.topq, tv, ti);
       const bool need = gi >= 0 && bo_better(acq, gi, tv, ti);
       if (__ballot(need) != 0ull) {
-        // acquisition.py:137-139, exact f64 coordinates; lane group g checks points g, g+4, ...
-        bool hit = false;
-        for (int e = g; e < ne; e += 4) {
-          const double* r = es + (size_t)e * DIM;
-          bool eq = true;
-#pragma unroll
-          for (int k = 0; k < DIM; ++k) eq = eq && (r[k] == c[k]);
-          hit = hit || eq;
-        }
+        // acquisition.py:137-139, exact f64 coordinates (hash probe + exact comparison)
+        const bool hit = valid && bo_hash_contains(a.hkeys, a.hidx, a.hmask, es, DIM, c, DIM);
         const unsigned long long hb = __ballot(hit);
         if (((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull) gi = -1;
       }

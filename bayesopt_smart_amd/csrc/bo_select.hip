@@ -107,6 +107,11 @@ struct SelArgs {
   long long grid_lo[BO_MAX_DIM], grid_shape[BO_MAX_DIM];
   const double* excl;
   const uint32_t* bitmap;   // grid kind: bit j set iff local candidate j is excluded (else NULL)
+  // explicit / Sobol kinds: open-addressing hash set of the evaluated points (keys: a hash of the
+  // coordinate bits, 0 = empty; idx: the point's row), NULL when it does not fit the workspace
+  const unsigned long long* hkeys;
+  const int* hidx;
+  unsigned int hmask;
   TopEntry* partial;
   SobolArgs sob;            // kind BO_CAND_SOBOL
 };
@@ -127,6 +132,30 @@ __global__ void excl_bitmap_kernel(uint32_t* __restrict__ bm, SelArgs a) {
   if (j >= 0 && j < a.n_cand) atomicOr(bm + (j >> 5), 1u << (j & 31));
 }
 
+__global__ void excl_hash_kernel(unsigned long long* __restrict__ keys, int* __restrict__ idx,
+                                 unsigned int mask, const double* __restrict__ excl, int n_excl, int dim) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_excl) return;
+  const unsigned long long key = bo_point_key(excl + (long long)e * dim, dim);
+  if (key != 0ull) bo_hash_insert(keys, idx, mask, key, e);
+}
+
+__device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int k);
+
+// candidate j equal (every coordinate) to an evaluated point?  Hash probe when the set is
+// hashed, else the O(n_excl) scan.
+__device__ __forceinline__ bool cand_excluded(const SelArgs& a, long long j) {
+  double c[BO_MAX_DIM];
+  for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
+  if (a.hkeys) return bo_hash_contains(a.hkeys, a.hidx, a.hmask, a.excl, a.dim, c, a.dim);
+  for (int e = 0; e < a.n_excl; ++e) {
+    bool eq = true;
+    for (int k = 0; k < a.dim; ++k) eq = eq && (a.excl[(long long)e * a.dim + k] == c[k]);
+    if (eq) return true;
+  }
+  return false;
+}
+
 __device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int k) {
   if (a.kind == BO_CAND_I64) return (double)((const long long*)a.cand)[j * a.dim + k];
   if (a.kind == BO_CAND_F64) return ((const double*)a.cand)[j * a.dim + k];
@@ -139,12 +168,7 @@ __device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int 
 // grid-stride over candidates; each wave folds 64 candidates per step into its running
 // top-q (4 inserts of 16), then writes its list to `partial`.
 __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
-  __shared__ double ex[1024 * BO_MAX_DIM];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n_lds = a.n_excl <= 1024 ? a.n_excl : 0;
-  for (int t = threadIdx.x; t < n_lds * a.dim; t += blockDim.x) ex[t] = a.excl[t];
-  __syncthreads();
-  const double* exs = n_lds ? ex : a.excl;
   double lv = -__builtin_inf();
   long long li = -1;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -166,15 +190,7 @@ __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
     if (a.bitmap) {
       if (gi >= 0 && ((a.bitmap[j >> 5] >> (j & 31)) & 1u)) gi = -1;
     } else if (__ballot(need) != 0ull && need) {
-      double c[BO_MAX_DIM];
-      for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
-      bool hit = false;
-      for (int e = 0; e < a.n_excl && !hit; ++e) {
-        bool eq = true;
-        for (int k = 0; k < a.dim; ++k) eq = eq && (exs[e * a.dim + k] == c[k]);
-        hit = eq;
-      }
-      if (hit) gi = -1;
+      if (cand_excluded(a, j)) gi = -1;
     }
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
@@ -196,8 +212,8 @@ __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
 // coalesced grid-stride sweep -- almost every element is rejected by one comparison with the
 // thread's Q-th entry; evaluated points are skipped by the grid bitmap, or (explicit sets) by
 // an exact coordinate test run only for elements that would enter the list -- then the wave
-// and the workgroup reduce their lists by Q rounds of arg-best (shuffles; the winner's owner
-// pops it), and bo_argbest_merge_kernel merges the workgroups' lists.
+// (wave_lists_topq: threshold set + ranks) and the workgroup (ranks of the 4 wave lists)
+// reduce the lists to the workgroup's top-q, and bo_topq_merge_kernel merges those.
 // M > 0 fuses the exact hypervolume improvement of bo_hvi.hip into the sweep: the acquisition
 // of candidate i is computed from its M UCB values and the boxes (wave-uniform, scalar loads),
 // written to acq, and selected in the same pass (one HBM read of the UCB arrays in total).
@@ -225,9 +241,80 @@ __device__ __forceinline__ void lane_insert(double (&v)[Q], long long (&ix)[Q], 
   }
 }
 
+// The top-q (q <= Q) of a wave's per-lane sorted lists, into out[0..q-1] (LDS):
+//   T = the best of the lanes' q-th entries; S = the entries not worse than T -- a prefix of
+//   every lane's list, normally about q .. 2q entries -- compacted into buf (64 entries, LDS)
+//   by one ballot per list slot, each ranked by a scan of S.  |S| > 64 (fewer than q valid
+//   entries per lane, or mass ties): q rounds of a wave arg-best, the owner popping its head.
+// (Round 1 ran Q arg-best rounds at the wave and again at the workgroup level: 6 shuffle
+// stages of (value, index) pairs per round.)  Called by all waves of the workgroup together.
+constexpr int BO_SEL_Q = 16;
+template <int Q>
+__device__ __forceinline__ void wave_lists_topq(double (&v)[Q], long long (&ix)[Q], int q,
+                                                TopEntry* buf, TopEntry* out) {
+  const int lane = threadIdx.x & 63;
+  double bv = -__builtin_inf();
+  long long bi = -1;
+#pragma unroll
+  for (int k = 0; k < Q; ++k)
+    if (k == q - 1) { bv = v[k]; bi = ix[k]; }
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) {
+    const double ov = __shfl_xor(bv, m, 64);
+    const long long oi = __shfl_xor(bi, m, 64);
+    if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  int c = 0;                                          // length of this lane's prefix in S
+#pragma unroll
+  for (int k = 0; k < Q; ++k)
+    if (k < q && ix[k] >= 0 && !bo_better(bv, bi, v[k], ix[k])) c = k + 1;
+  int total = 0;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {
+    if (k >= q) break;
+    const unsigned long long b = __ballot(c > k);
+    const int off = total + __popcll(b & lt);
+    if (c > k && off < 64) { buf[off].v = v[k]; buf[off].i = ix[k]; }
+    total += __popcll(b);
+  }
+  __syncthreads();
+  if (total <= 64) {
+    if (lane < total) {
+      const TopEntry me = buf[lane];
+      int rank = 0;
+      for (int m = 0; m < total; ++m) rank += bo_better(buf[m].v, buf[m].i, me.v, me.i) ? 1 : 0;
+      if (rank < q) out[rank] = me;
+    } else if (lane < q) {
+      out[lane].v = -__builtin_inf();
+      out[lane].i = -1;
+    }
+    return;
+  }
+#pragma unroll 1
+  for (int r = 0; r < q; ++r) {
+    double hv = v[0];
+    long long hi = ix[0];
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+      const double ov = __shfl_xor(hv, m, 64);
+      const long long oi = __shfl_xor(hi, m, 64);
+      if (bo_better(ov, oi, hv, hi)) { hv = ov; hi = oi; }
+    }
+    if (lane == 0) { out[r].v = hv; out[r].i = hi; }
+    if (hi >= 0 && ix[0] == hi) {
+#pragma unroll
+      for (int k = 0; k + 1 < Q; ++k) { v[k] = v[k + 1]; ix[k] = ix[k + 1]; }
+      v[Q - 1] = -__builtin_inf();
+      ix[Q - 1] = -1;
+    }
+  }
+}
+
 template <int Q, int M>
 __global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
-  __shared__ TopEntry wl[4 * Q];
+  __shared__ TopEntry wl[4 * BO_SEL_Q];
+  __shared__ TopEntry wbuf[4 * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double v[Q];
   long long ix[Q];
@@ -277,57 +364,28 @@ __global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
       const long long gi = a.cand_offset + j;
       if ((bits[u] >> (j & 31)) & 1u) continue;
       if (!bo_better(val[u], gi, v[Q - 1], ix[Q - 1])) continue;
-      if (!a.bitmap && a.n_excl > 0) {
-        double c[BO_MAX_DIM];
-        for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
-        bool hit = false;
-        for (int e = 0; e < a.n_excl && !hit; ++e) {
-          bool eq = true;
-          for (int k = 0; k < a.dim; ++k) eq = eq && (a.excl[(long long)e * a.dim + k] == c[k]);
-          hit = eq;
-        }
-        if (hit) continue;
-      }
+      if (!a.bitmap && a.n_excl > 0 && cand_excluded(a, j)) continue;
       lane_insert<Q>(v, ix, val[u], gi);
     }
   }
-  // wave: Q rounds of arg-best over the lanes' heads; the owner pops its head
-#pragma unroll 1
-  for (int r = 0; r < Q; ++r) {
-    double bv = v[0];
-    long long bi = ix[0];
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) {
-      const double ov = __shfl_xor(bv, m, 64);
-      const long long oi = __shfl_xor(bi, m, 64);
-      if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) { wl[wave * Q + r].v = bv; wl[wave * Q + r].i = bi; }
-    if (bi >= 0 && ix[0] == bi) {
-#pragma unroll
-      for (int k = 0; k + 1 < Q; ++k) { v[k] = v[k + 1]; ix[k] = ix[k + 1]; }
-      v[Q - 1] = -__builtin_inf();
-      ix[Q - 1] = -1;
-    }
-  }
+  // wave, then workgroup: the top-q of the lanes' lists (wave_lists_topq), then of the 4 wave
+  // lists (rank by LDS scan); the workgroup's list goes to `partial` ([blocks][q])
+  wave_lists_topq<Q>(v, ix, a.topq, wbuf + wave * 64, wl + wave * BO_SEL_Q);
   __syncthreads();
-  // workgroup: wave 0 merges the 4 wave lists (4 Q <= 64 entries, one per lane)
   if (wave == 0) {
-    double ev = lane < 4 * Q ? wl[lane].v : -__builtin_inf();
-    long long ei = lane < 4 * Q ? wl[lane].i : -1;
-    TopEntry* dst = a.partial + (size_t)blockIdx.x * Q;
-#pragma unroll 1
-    for (int r = 0; r < Q; ++r) {
-      double bv = ev;
-      long long bi = ei;
-#pragma unroll
-      for (int m = 32; m > 0; m >>= 1) {
-        const double ov = __shfl_xor(bv, m, 64);
-        const long long oi = __shfl_xor(bi, m, 64);
-        if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    const int n = 4 * a.topq;
+    TopEntry* dst = a.partial + (size_t)blockIdx.x * a.topq;
+    if (lane < a.topq) { dst[lane].v = -__builtin_inf(); dst[lane].i = -1; }
+    if (lane < n) {
+      const TopEntry me = wl[(lane / a.topq) * BO_SEL_Q + lane % a.topq];
+      if (me.i >= 0) {
+        int rank = 0;
+        for (int m = 0; m < n; ++m) {
+          const TopEntry o = wl[(m / a.topq) * BO_SEL_Q + m % a.topq];
+          rank += bo_better(o.v, o.i, me.v, me.i) ? 1 : 0;
+        }
+        if (rank < a.topq) dst[rank] = me;
       }
-      if (lane == 0) { dst[r].v = bv; dst[r].i = bi; }
-      if (bi >= 0 && ei == bi) { ev = -__builtin_inf(); ei = -1; }
     }
   }
 }
@@ -339,35 +397,6 @@ int launch_select_lane(const SelArgs& a, const HviIn& h, int q, int blocks, hipS
   else hipLaunchKernelGGL((select_lane_kernel<16, M>), dim3(blocks), dim3(256), 0, s, a, h);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
-}
-
-__global__ __launch_bounds__(1024) void merge_kernel(const TopEntry* __restrict__ lists,
-                                                     int n_lists, int q, double* __restrict__ out_v,
-                                                     long long* __restrict__ out_i) {
-  __shared__ TopEntry stage[16 * BO_MAX_TOPQ];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  double lv = -__builtin_inf();
-  long long li = -1;
-  const long long total = (long long)n_lists * q;
-  for (long long base = (long long)wave * 16; base < total; base += (long long)nw * 16) {
-    double nv = -__builtin_inf();
-    long long ni = -1;
-    if (lane < 16 && base + lane < total) { nv = lists[base + lane].v; ni = lists[base + lane].i; }
-    bo_wave_topq_insert(lv, li, nv, ni, q);
-  }
-  if (lane < q) { stage[wave * q + lane].v = lv; stage[wave * q + lane].i = li; }
-  __syncthreads();
-  if (wave == 0) {
-    double fv = -__builtin_inf();
-    long long fi = -1;
-    for (int base = 0; base < nw * q; base += 16) {
-      double nv = -__builtin_inf();
-      long long ni = -1;
-      if (lane < 16 && base + lane < nw * q) { nv = stage[base + lane].v; ni = stage[base + lane].i; }
-      bo_wave_topq_insert(fv, fi, nv, ni, q);
-    }
-    if (lane < q) { out_v[lane] = fv; out_i[lane] = fi; }
-  }
 }
 
 // --------------------------------------------------------------------------- Pareto
@@ -557,6 +586,22 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
     hipLaunchKernelGGL(excl_bitmap_kernel, dim3((unsigned)((n_excl + 255) / 256)), dim3(256), 0, s, bm, a);
     BO_CHECK_HIP(hipGetLastError());
     a.bitmap = bm;
+  } else if (kind != BO_CAND_GRID && n_excl > 0 && n_cand > 0) {
+    // explicit / Sobol: hash set of the evaluated points in the bitmap's (unused) region when
+    // it fits -- 2 n_excl .. 4 n_excl slots of 12 B -- else the exclusion scans the points
+    const unsigned int slots = bo_hash_slots(n_excl);
+    const size_t region = ((size_t)n_cand + 31) / 32 * 4;
+    if ((size_t)slots * 12 <= region) {
+      unsigned long long* keys = (unsigned long long*)((char*)ws + sel_lists_bytes(topq));
+      int* idx = (int*)(keys + slots);
+      BO_CHECK_HIP(hipMemsetAsync(keys, 0, (size_t)slots * 8, s));
+      hipLaunchKernelGGL(excl_hash_kernel, dim3((unsigned)((n_excl + 255) / 256)), dim3(256), 0, s,
+                         keys, idx, slots - 1, excl, (int)n_excl, dim);
+      BO_CHECK_HIP(hipGetLastError());
+      a.hkeys = keys;
+      a.hidx = idx;
+      a.hmask = slots - 1;
+    }
   }
   long long blocks = (n_cand + 255) / 256;
   if (topq <= 16) {
@@ -578,9 +623,8 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
       default: return BO_ERR_UNSUPPORTED;
     }
     if (st != BO_OK) return st;
-    const int Q = topq <= 4 ? 4 : (topq <= 8 ? 8 : 16);
-    hipLaunchKernelGGL(bo_argbest_merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
-                       blocks * Q, topq, top_val, (long long*)top_idx);
+    hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
+                       blocks, topq, top_val, (long long*)top_idx);
     BO_CHECK_HIP(hipGetLastError());
     return BO_OK;
   }
@@ -591,8 +635,8 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(select_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
   BO_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
-                     (int)blocks * 4, topq, top_val, (long long*)top_idx);
+  hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
+                     blocks * 4, topq, top_val, (long long*)top_idx);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
 }

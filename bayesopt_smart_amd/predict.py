@@ -188,6 +188,8 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     ``top_rec`` (optional f64 device tensor [2 topq]): the selection is written into it as one
     16-B-per-entry record block -- values in [:topq], int64 indices (bit pattern) in [topq:] --
     so that the multi-GPU exchange is ONE all_gather of it (distributed.exchange_topq_rec).
+    A pinned host tensor is accepted too: the merge kernel then writes the selection straight
+    into host memory (one shard: no device-to-host copy after the call).
 
     ``prepare=True`` returns a PreparedPredict instead of launching: calling it launches this
     call again (same buffers), without re-validating.
@@ -233,9 +235,11 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     desc.ld_out = ld_out or count
     if topq:
         if top_rec is not None:
+            on_dev = top_rec.device == dev or (top_rec.device.type == "cpu" and top_rec.is_pinned())
             if top_rec.dtype != F64 or top_rec.numel() != 2 * topq or not top_rec.is_contiguous() \
-                    or top_rec.device != dev:
-                raise ValueError("top_rec must be a contiguous f64 device tensor of 2 * topq entries")
+                    or not on_dev:
+                raise ValueError("top_rec must be a contiguous f64 tensor of 2 * topq entries, on "
+                                 "the device or in pinned host memory")
             res["top_val"] = top_rec[:topq]
             res["top_idx"] = top_rec[topq:].view(torch.int64)
         else:

@@ -372,7 +372,11 @@ def main():
                           device=dev) for k in outputs}
     # the top-q exchange: each rank's list as ONE block of 16-B records (values, int64 indices),
     # one all_gather of P * q * 16 bytes
-    rec = torch.empty(2 * q, dtype=torch.float64, device=dev)
+    # (one shard: the record block lives in pinned host memory and the merge kernel writes the
+    # selection straight into it -- no device-to-host copy launch per step)
+    rec = torch.empty(2 * q, dtype=torch.float64, device=dev) if world > 1 or args.acq == "hvi" \
+        else torch.empty(2 * q, dtype=torch.float64).pin_memory()
+    rec_np = rec.numpy() if rec.device.type == "cpu" else None
     gath = torch.empty(world * 2 * q, dtype=torch.float64, device=dev)
 
     hvi_ev = []
@@ -427,8 +431,12 @@ def main():
             g = gath.view(world, 2 * q).cpu()
             return bo.merge_topq(g[:, :q].numpy(), g[:, q:].contiguous().view(torch.int64).numpy(), q)
         # one shard: the device list is already merged and in selection order
-        g = rec.cpu()
-        v, i = g[:q].numpy(), g[q:].view(torch.int64).numpy()
+        if rec_np is not None:
+            torch.cuda.current_stream(dev).synchronize()
+            v, i = rec_np[:q].copy(), rec_np[q:].view(np.int64).copy()
+        else:
+            g = rec.cpu()
+            v, i = g[:q].numpy(), g[q:].view(torch.int64).numpy()
         return v[i >= 0], i[i >= 0]
 
     for _ in range(args.warmup):
@@ -520,11 +528,14 @@ def main():
                                         "method": f"bo_box_volume_sum over this rank's share of the "
                                                   f"{n_boxes[0]} boxes + all_reduce(SUM) over {world} rank(s)"}
             res["hvi_select"] = {"kernels": f"select_lane_kernel<{4 if q <= 4 else 8 if q <= 8 else 16}, {n_obj}> "
-                                            "+ bo_argbest_merge_kernel (exact HVI + top-q, one pass)",
+                                            "+ bo_topq_merge_kernel (exact HVI + top-q, one pass)",
                                  "ms": hms, "n_boxes": n_boxes[0], "front_points": int(front_y.shape[0]),
                                  "bytes_per_candidate": 8 * n_obj + 8,
                                  "achieved_GBps": hb / (hms * 1e-3) / 1e9,
                                  "hbm_frac": hb / (hms * 1e-3) / 1e9 / 8000.0}
+        if args.acq == "sum_ucb" and q <= 16:
+            res["select_standalone"] = standalone_select(lib, bo, out["acq"], cands, offset, per_rank, xd,
+                                                         q, dev, sel[1])
         if world == 1 and not args.no_cpu_baseline and args.acq == "sum_ucb":
             if cand[0] == "grid":
                 side = cand[2]
@@ -553,6 +564,43 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def standalone_select(lib, bo, acq, cands, offset, n, xd, q, dev, fused_sel, reps=20):
+    """bo_select_topq (select_next_batch over a stored acquisition array, acquisition.py:116-144)
+    on this shard's acq array from the timed run, with the evaluated points excluded: HIP-event
+    time per call (one-pass selection kernel + the final merge), its HBM rate on the 8 B per
+    candidate it must read, and whether it selects what the fused kernel selected.  Outside the
+    timed region."""
+    import ctypes
+    import torch
+    ws = torch.empty(lib.bo_select_topq_workspace_size(n, q), dtype=torch.uint8, device=dev)
+    tv = torch.empty(q, dtype=torch.float64, device=dev)
+    ti = torch.empty(q, dtype=torch.int64, device=dev)
+    glo = (ctypes.c_int64 * 8)(*((list(cands.lo) if cands.lo else []) + [0] * (8 - len(cands.lo or []))))
+    gsh = (ctypes.c_int64 * 8)(*((list(cands.shape) if cands.shape else []) + [1] * (8 - len(cands.shape or []))))
+    carg = cands.tensor[offset:].data_ptr() if cands.kind in ("i64", "f64") else cands.cand_arg
+    strm = bo.device.stream_handle(dev)
+
+    def call():
+        bo._lib.check(lib.bo_select_topq(acq.data_ptr(), n, cands.kind_code, carg, glo, gsh, cands.dim,
+                                         offset, xd.data_ptr(), xd.shape[0], q, tv.data_ptr(),
+                                         ti.data_ptr(), ws.data_ptr(), ws.numel(), strm), "select")
+    call()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    got = ti.cpu().numpy()
+    return {"kernels": f"select_lane_kernel<{4 if q <= 4 else 8 if q <= 8 else 16}, 0> + bo_topq_merge_kernel"
+                       + (" (+ exclusion bitmap)" if cands.kind == "grid" else ""),
+            "ms": ms, "bytes": 8 * n, "achieved_GBps": 8 * n / (ms * 1e-3) / 1e9,
+            "hbm_frac": 8 * n / (ms * 1e-3) / 1e9 / 8000.0,
+            "matches_fused_selection": bool(np.array_equal(got[got >= 0], np.asarray(fused_sel)))}
 
 
 def _rows_in(pts, x):
