@@ -106,31 +106,16 @@ struct SelArgs {
   const void* cand;
   long long grid_lo[BO_MAX_DIM], grid_shape[BO_MAX_DIM];
   const double* excl;
-  const uint32_t* bitmap;   // grid kind: bit j set iff local candidate j is excluded (else NULL)
-  // explicit / Sobol kinds: open-addressing hash set of the evaluated points (keys: a hash of the
-  // coordinate bits, 0 = empty; idx: the point's row), NULL when it does not fit the workspace
+  // open-addressing hash set of the evaluated points (keys: bo_point_key, 0 = empty; idx: the
+  // point's row): built per workgroup in LDS (lds_slots > 0, select_lane_kernel), else in the
+  // workspace (hkeys), else NULL (the exclusion scans the points)
+  int lds_slots;
   const unsigned long long* hkeys;
   const int* hidx;
   unsigned int hmask;
   TopEntry* partial;
   SobolArgs sob;            // kind BO_CAND_SOBOL
 };
-
-// Grid kind: mark the evaluated points that lie on this shard of the grid in a bitmap over the
-// shard's local indices (a point equals a grid candidate iff every coordinate is the integer
-// lo_k + v_k with 0 <= v_k < shape_k: the reference's all-d `==`, acquisition.py:137-139).
-__global__ void excl_bitmap_kernel(uint32_t* __restrict__ bm, SelArgs a) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.n_excl) return;
-  long long lin = 0;
-  for (int k = 0; k < a.dim; ++k) {
-    const double v = a.excl[(long long)e * a.dim + k] - (double)a.grid_lo[k];
-    if (!(v >= 0.0) || v >= (double)a.grid_shape[k] || v != floor(v)) return;
-    lin = lin * a.grid_shape[k] + (long long)v;
-  }
-  const long long j = lin - a.cand_offset;
-  if (j >= 0 && j < a.n_cand) atomicOr(bm + (j >> 5), 1u << (j & 31));
-}
 
 __global__ void excl_hash_kernel(unsigned long long* __restrict__ keys, int* __restrict__ idx,
                                  unsigned int mask, const double* __restrict__ excl, int n_excl, int dim) {
@@ -142,12 +127,14 @@ __global__ void excl_hash_kernel(unsigned long long* __restrict__ keys, int* __r
 
 __device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int k);
 
-// candidate j equal (every coordinate) to an evaluated point?  Hash probe when the set is
-// hashed, else the O(n_excl) scan.
-__device__ __forceinline__ bool cand_excluded(const SelArgs& a, long long j) {
+// candidate j equal (every coordinate) to an evaluated point?  Hash probe when a table is
+// given, else the O(n_excl) scan.
+__device__ __forceinline__ bool cand_excluded(const SelArgs& a, long long j,
+                                              const unsigned long long* hk, const int* hi,
+                                              unsigned int hm) {
   double c[BO_MAX_DIM];
   for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
-  if (a.hkeys) return bo_hash_contains(a.hkeys, a.hidx, a.hmask, a.excl, a.dim, c, a.dim);
+  if (hk) return bo_hash_contains(hk, hi, hm, a.excl, a.dim, c, a.dim);
   for (int e = 0; e < a.n_excl; ++e) {
     bool eq = true;
     for (int k = 0; k < a.dim; ++k) eq = eq && (a.excl[(long long)e * a.dim + k] == c[k]);
@@ -187,10 +174,8 @@ __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
     const double tv = __shfl(lv, a.topq - 1, 64);
     const long long ti = __shfl(li, a.topq - 1, 64);
     const bool need = a.n_excl > 0 && gi >= 0 && bo_better(v, gi, tv, ti);
-    if (a.bitmap) {
-      if (gi >= 0 && ((a.bitmap[j >> 5] >> (j & 31)) & 1u)) gi = -1;
-    } else if (__ballot(need) != 0ull && need) {
-      if (cand_excluded(a, j)) gi = -1;
+    if (__ballot(need) != 0ull && need) {
+      if (cand_excluded(a, j, a.hkeys, a.hidx, a.hmask)) gi = -1;
     }
 #pragma unroll
     for (int grp = 0; grp < 4; ++grp) {
@@ -208,12 +193,13 @@ __global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // Selection for q <= 16 (every batch the reference's demos use), ONE pass at HBM rate:
-// every thread keeps its own sorted top-Q (Q = 4 / 8 / 16 >= q) in registers over a
-// coalesced grid-stride sweep -- almost every element is rejected by one comparison with the
-// thread's Q-th entry; evaluated points are skipped by the grid bitmap, or (explicit sets) by
-// an exact coordinate test run only for elements that would enter the list -- then the wave
-// (wave_lists_topq: threshold set + ranks) and the workgroup (ranks of the 4 wave lists)
-// reduce the lists to the workgroup's top-q, and bo_topq_merge_kernel merges those.
+// every thread keeps its own sorted top-Q (Q = 8 / 16 / 24, at least q + 4) in registers over
+// a coalesced grid-stride sweep -- almost every element is rejected by one comparison with the
+// thread's Q-th entry.  The exclusion of evaluated points is deferred to the Q list entries of
+// each thread (hash set of the points, built in LDS by every workgroup), so the sweep reads
+// nothing but the acquisition values.  Then the wave (wave_lists_topq: threshold set + ranks)
+// and the workgroup (ranks of the 4 wave lists) reduce the lists to the workgroup's top-q, and
+// bo_topq_merge_kernel merges those.
 // M > 0 fuses the exact hypervolume improvement of bo_hvi.hip into the sweep: the acquisition
 // of candidate i is computed from its M UCB values and the boxes (wave-uniform, scalar loads),
 // written to acq, and selected in the same pass (one HBM read of the UCB arrays in total).
@@ -249,25 +235,43 @@ __device__ __forceinline__ void lane_insert(double (&v)[Q], long long (&ix)[Q], 
 // (Round 1 ran Q arg-best rounds at the wave and again at the workgroup level: 6 shuffle
 // stages of (value, index) pairs per round.)  Called by all waves of the workgroup together.
 constexpr int BO_SEL_Q = 16;
-template <int Q>
+// `excluded(idx)` tests a list entry (global index) against the evaluated points; `purge()`
+// drops every excluded entry of the calling lane's list (and rebuilds the list if too few
+// remain).  The exclusion is only tested on S: when no entry of S is excluded, S also holds the
+// top-q of the non-excluded elements; otherwise (rare) every lane purges and T, S are redone.
+template <int Q, class Excl, class Purge>
 __device__ __forceinline__ void wave_lists_topq(double (&v)[Q], long long (&ix)[Q], int q,
-                                                TopEntry* buf, TopEntry* out) {
+                                                TopEntry* buf, TopEntry* out, bool check,
+                                                Excl excluded, Purge purge) {
   const int lane = threadIdx.x & 63;
-  double bv = -__builtin_inf();
-  long long bi = -1;
+  double bv;
+  long long bi;
+  int c;
+  for (;;) {
+    bv = -__builtin_inf();
+    bi = -1;
 #pragma unroll
-  for (int k = 0; k < Q; ++k)
-    if (k == q - 1) { bv = v[k]; bi = ix[k]; }
+    for (int k = 0; k < Q; ++k)
+      if (k == q - 1) { bv = v[k]; bi = ix[k]; }
 #pragma unroll
-  for (int m = 32; m > 0; m >>= 1) {
-    const double ov = __shfl_xor(bv, m, 64);
-    const long long oi = __shfl_xor(bi, m, 64);
-    if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    for (int m = 32; m > 0; m >>= 1) {
+      const double ov = __shfl_xor(bv, m, 64);
+      const long long oi = __shfl_xor(bi, m, 64);
+      if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    c = 0;                                            // length of this lane's prefix in S
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+      if (k < q && ix[k] >= 0 && !bo_better(bv, bi, v[k], ix[k])) c = k + 1;
+    if (!check) break;
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+      if (k < c) bad = bad || excluded(ix[k]);
+    if (__ballot(bad) == 0ull) break;
+    purge();
+    check = false;
   }
-  int c = 0;                                          // length of this lane's prefix in S
-#pragma unroll
-  for (int k = 0; k < Q; ++k)
-    if (k < q && ix[k] >= 0 && !bo_better(bv, bi, v[k], ix[k])) c = k + 1;
   int total = 0;
   const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
@@ -313,64 +317,115 @@ __device__ __forceinline__ void wave_lists_topq(double (&v)[Q], long long (&ix)[
 
 template <int Q, int M>
 __global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lkeys[];   // [lds_slots], then idx
   __shared__ TopEntry wl[4 * BO_SEL_Q];
   __shared__ TopEntry wbuf[4 * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the evaluated points' hash set, in LDS when small (built by every workgroup: no extra
+  // launches), else the workspace table, else none (scan)
+  const unsigned long long* hk = a.hkeys;
+  const int* hi = a.hidx;
+  unsigned int hm = a.hmask;
+  if (a.lds_slots > 0) {
+    int* lidx = (int*)(lkeys + a.lds_slots);
+    for (int t = tid; t < a.lds_slots; t += blockDim.x) lkeys[t] = 0ull;
+    __syncthreads();
+    for (int e = tid; e < a.n_excl; e += blockDim.x) {
+      const unsigned long long key = bo_point_key(a.excl + (long long)e * a.dim, a.dim);
+      if (key != 0ull) bo_hash_insert(lkeys, lidx, (unsigned int)a.lds_slots - 1, key, e);
+    }
+    __syncthreads();
+    hk = lkeys;
+    hi = lidx;
+    hm = (unsigned int)a.lds_slots - 1;
+  }
   double v[Q];
   long long ix[Q];
-#pragma unroll
-  for (int k = 0; k < Q; ++k) { v[k] = -__builtin_inf(); ix[k] = -1; }
   const long long stride = (long long)gridDim.x * blockDim.x;
   // U elements per thread and sweep step, all loaded before any is processed (the loads of a
-  // step are in flight together; the loop body alone would expose one latency per element)
+  // step are in flight together; the loop body alone would expose one latency per element).
+  // The sweep itself ignores the exclusion (check = false): see below.
   constexpr int U = 4;
-  for (long long j0 = (long long)blockIdx.x * blockDim.x + tid; j0 < a.n_cand; j0 += U * stride) {
-    double val[U];
-    uint32_t bits[U];
+  auto sweep = [&](bool check) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long j = j0 + u * stride;
-      const bool in = j < a.n_cand;
-      bits[u] = (in && a.bitmap) ? a.bitmap[j >> 5] : 0u;
-      if constexpr (M == 0) {
-        val[u] = in ? a.acq[j] : 0.0;
-      } else {
-        double p[M];
-        bool nan = false;
+    for (int k = 0; k < Q; ++k) { v[k] = -__builtin_inf(); ix[k] = -1; }
+    for (long long j0 = (long long)blockIdx.x * blockDim.x + tid; j0 < a.n_cand; j0 += U * stride) {
+      double val[U];
 #pragma unroll
-        for (int k = 0; k < M; ++k) {
-          p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
-          nan = nan || (p[k] != p[k]);
-        }
-        double hv = 0.0;
-        const double* b = h.boxes;
-        for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
-          double w = 1.0;
+      for (int u = 0; u < U; ++u) {
+        const long long j = j0 + u * stride;
+        const bool in = j < a.n_cand;
+        if constexpr (M == 0) {
+          val[u] = in ? a.acq[j] : 0.0;
+        } else {
+          double p[M];
+          bool nan = false;
 #pragma unroll
           for (int k = 0; k < M; ++k) {
-            const double hi = p[k] < b[M + k] ? p[k] : b[M + k];
-            w *= fmax(hi - b[k], 0.0);
+            p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
+            nan = nan || (p[k] != p[k]);
           }
-          hv += w;
+          double hv = 0.0;
+          const double* b = h.boxes;
+          for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
+            double w = 1.0;
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+              const double hi2 = p[k] < b[M + k] ? p[k] : b[M + k];
+              w *= fmax(hi2 - b[k], 0.0);
+            }
+            hv += w;
+          }
+          val[u] = nan ? __builtin_nan("") : hv;
+          if (in) h.acq_out[j] = val[u];
         }
-        val[u] = nan ? __builtin_nan("") : hv;
-        if (in) h.acq_out[j] = val[u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long j = j0 + u * stride;
+        if (j >= a.n_cand) break;
+        const long long gi = a.cand_offset + j;
+        if (!bo_better(val[u], gi, v[Q - 1], ix[Q - 1])) continue;
+        if (check && cand_excluded(a, j, hk, hi, hm)) continue;
+        lane_insert<Q>(v, ix, val[u], gi);
       }
     }
+  };
+  sweep(false);
+  // Deferred exclusion (acquisition.py:137-139): tested on the wave's threshold set S only
+  // (wave_lists_topq); purge() runs when an entry of S is an evaluated point.  Without its
+  // excluded entries a list still holds its thread's best non-excluded elements; it needs q of
+  // them unless it held every element of the thread (Q - q >= 4), else the thread rescans with
+  // per-element tests.
+  auto excluded = [&](long long gi) { return gi >= 0 && cand_excluded(a, gi - a.cand_offset, hk, hi, hm); };
+  auto purge = [&]() {
+    const bool full = ix[Q - 1] >= 0;
+    bool ex[Q];
+    int removed = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long j = j0 + u * stride;
-      if (j >= a.n_cand) break;
-      const long long gi = a.cand_offset + j;
-      if ((bits[u] >> (j & 31)) & 1u) continue;
-      if (!bo_better(val[u], gi, v[Q - 1], ix[Q - 1])) continue;
-      if (!a.bitmap && a.n_excl > 0 && cand_excluded(a, j)) continue;
-      lane_insert<Q>(v, ix, val[u], gi);
+    for (int k = 0; k < Q; ++k) {
+      ex[k] = excluded(ix[k]);
+      removed += ex[k] ? 1 : 0;
     }
-  }
+    if (removed == 0) return;
+    if (full && Q - removed < a.topq) {
+      sweep(true);
+      return;
+    }
+#pragma unroll
+    for (int k = Q - 1; k >= 0; --k) {
+      if (ex[k]) {
+#pragma unroll
+        for (int t = k; t + 1 < Q; ++t) { v[t] = v[t + 1]; ix[t] = ix[t + 1]; }
+        v[Q - 1] = -__builtin_inf();
+        ix[Q - 1] = -1;
+      }
+    }
+  };
   // wave, then workgroup: the top-q of the lanes' lists (wave_lists_topq), then of the 4 wave
   // lists (rank by LDS scan); the workgroup's list goes to `partial` ([blocks][q])
-  wave_lists_topq<Q>(v, ix, a.topq, wbuf + wave * 64, wl + wave * BO_SEL_Q);
+  wave_lists_topq<Q>(v, ix, a.topq, wbuf + wave * 64, wl + wave * BO_SEL_Q, a.n_excl > 0,
+                     excluded, purge);
   __syncthreads();
   if (wave == 0) {
     const int n = 4 * a.topq;
@@ -392,9 +447,10 @@ __global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
 
 template <int M>
 int launch_select_lane(const SelArgs& a, const HviIn& h, int q, int blocks, hipStream_t s) {
-  if (q <= 4) hipLaunchKernelGGL((select_lane_kernel<4, M>), dim3(blocks), dim3(256), 0, s, a, h);
-  else if (q <= 8) hipLaunchKernelGGL((select_lane_kernel<8, M>), dim3(blocks), dim3(256), 0, s, a, h);
-  else hipLaunchKernelGGL((select_lane_kernel<16, M>), dim3(blocks), dim3(256), 0, s, a, h);
+  const size_t lds = (size_t)a.lds_slots * 12;
+  if (q <= 4) hipLaunchKernelGGL((select_lane_kernel<8, M>), dim3(blocks), dim3(256), lds, s, a, h);
+  else if (q <= 12) hipLaunchKernelGGL((select_lane_kernel<16, M>), dim3(blocks), dim3(256), lds, s, a, h);
+  else hipLaunchKernelGGL((select_lane_kernel<24, M>), dim3(blocks), dim3(256), lds, s, a, h);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
 }
@@ -580,18 +636,15 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
     }
   a.excl = excl;
   a.partial = (TopEntry*)ws;
-  if (kind == BO_CAND_GRID && n_excl > 0 && n_cand > 0) {
-    uint32_t* bm = (uint32_t*)((char*)ws + sel_lists_bytes(topq));
-    BO_CHECK_HIP(hipMemsetAsync(bm, 0, ((size_t)n_cand + 31) / 32 * 4, s));
-    hipLaunchKernelGGL(excl_bitmap_kernel, dim3((unsigned)((n_excl + 255) / 256)), dim3(256), 0, s, bm, a);
-    BO_CHECK_HIP(hipGetLastError());
-    a.bitmap = bm;
-  } else if (kind != BO_CAND_GRID && n_excl > 0 && n_cand > 0) {
-    // explicit / Sobol: hash set of the evaluated points in the bitmap's (unused) region when
-    // it fits -- 2 n_excl .. 4 n_excl slots of 12 B -- else the exclusion scans the points
+  if (n_excl > 0 && n_cand > 0) {
+    // the evaluated points' hash set: per workgroup in LDS (<= 1024 points, one-pass kernel),
+    // else in the workspace region after the lists when it fits (2 n_excl .. 4 n_excl slots of
+    // 12 B), else none (the exclusion scans the points)
     const unsigned int slots = bo_hash_slots(n_excl);
     const size_t region = ((size_t)n_cand + 31) / 32 * 4;
-    if ((size_t)slots * 12 <= region) {
+    if (topq <= 16 && n_excl <= 1024) {
+      a.lds_slots = (int)slots;
+    } else if ((size_t)slots * 12 <= region) {
       unsigned long long* keys = (unsigned long long*)((char*)ws + sel_lists_bytes(topq));
       int* idx = (int*)(keys + slots);
       BO_CHECK_HIP(hipMemsetAsync(keys, 0, (size_t)slots * 8, s));

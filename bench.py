@@ -527,7 +527,7 @@ def main():
             res["front_hypervolume"] = {"value": hv_front, "reference_point": ref_pt.tolist(),
                                         "method": f"bo_box_volume_sum over this rank's share of the "
                                                   f"{n_boxes[0]} boxes + all_reduce(SUM) over {world} rank(s)"}
-            res["hvi_select"] = {"kernels": f"select_lane_kernel<{4 if q <= 4 else 8 if q <= 8 else 16}, {n_obj}> "
+            res["hvi_select"] = {"kernels": f"select_lane_kernel<{8 if q <= 4 else 16 if q <= 12 else 24}, {n_obj}> "
                                             "+ bo_topq_merge_kernel (exact HVI + top-q, one pass)",
                                  "ms": hms, "n_boxes": n_boxes[0], "front_points": int(front_y.shape[0]),
                                  "bytes_per_candidate": 8 * n_obj + 8,
@@ -596,8 +596,7 @@ def standalone_select(lib, bo, acq, cands, offset, n, xd, q, dev, fused_sel, rep
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     got = ti.cpu().numpy()
-    return {"kernels": f"select_lane_kernel<{4 if q <= 4 else 8 if q <= 8 else 16}, 0> + bo_topq_merge_kernel"
-                       + (" (+ exclusion bitmap)" if cands.kind == "grid" else ""),
+    return {"kernels": f"select_lane_kernel<{8 if q <= 4 else 16 if q <= 12 else 24}, 0> + bo_topq_merge_kernel",
             "ms": ms, "bytes": 8 * n, "achieved_GBps": 8 * n / (ms * 1e-3) / 1e9,
             "hbm_frac": 8 * n / (ms * 1e-3) / 1e9 / 8000.0,
             "matches_fused_selection": bool(np.array_equal(got[got >= 0], np.asarray(fused_sel)))}

@@ -150,6 +150,40 @@ def test_select_next_batch_large_batch_and_exhaustion(bo):
     np.testing.assert_array_equal(got, O.select_next_batch(cand, acq, ev, 500))
 
 
+@pytest.mark.parametrize("kind", ["grid", "f64"])
+@pytest.mark.parametrize("q", [3, 8, 16])
+def test_select_deferred_exclusion_paths(bo, kind, q):
+    """bo_select_topq's one-pass kernel tests the exclusion only on each wave's threshold set:
+    here the best candidates of the whole set are evaluated points, all in the list of ONE
+    thread of the grid-stride sweep (its elements j = t + k * stride), so that set is purged
+    and that thread rescans with per-element tests; plus evaluated points scattered over the
+    top of the order.  Exact selection order against numpy."""
+    import torch
+    side0, side1 = 2048, 1024
+    m = side0 * side1
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    stride = min((m + 255) // 256, 2 * cus, 512) * 256
+    rng = np.random.default_rng(q)
+    acq = rng.standard_normal(m)
+    hot = 7 + stride * np.arange(m // stride)              # thread 7's elements
+    acq[hot] = 100.0 + np.arange(hot.size)                  # the best of all, evaluated below
+    lin = np.arange(m)
+    cand_pts = np.stack([lin // side1, lin % side1], axis=1)
+    top = np.argsort(-acq, kind="stable")[:200]
+    scatter = top[hot.size::3][:20]                         # more evaluated points near the top
+    ev = cand_pts[np.concatenate([hot, scatter])].astype(np.float64)
+    if kind == "grid":
+        cands = bo.predict.CandidateSet.grid([(0, side0), (0, side1)])
+    else:
+        cands = bo.predict.CandidateSet.explicit(cand_pts.astype(np.float64))
+    got = bo.acquisition.select_indices(torch.tensor(acq, device="cuda"), cands, ev, q)
+    excl = np.zeros(m, dtype=bool)
+    excl[hot] = True
+    excl[scatter] = True
+    order = np.lexsort((lin, -np.where(excl, -np.inf, acq)))
+    np.testing.assert_array_equal(got, order[:q])
+
+
 def test_pareto_mask_bit_exact(bo):
     d = load_golden("g5_pareto")
     for key in d.files:
