@@ -149,12 +149,12 @@ def hypervolume_improvement_exact(ucb, front, reference_point, prior_mean, prior
 def hvi_select_indices(acquisition_values, ucb, y_vector, n_evaluations, reference_point, prior_mean,
                        prior_variance, cands, evaluated_points, batch_size):
     """The exact-HVI acquisition AND its batch selection in one device pass (bo_hvi_select_topq,
-    batch_size <= 16): acquisition_values (device, [M]) receives the HVI of every candidate's
+    batch_size <= BO_MAX_TOPQ): acquisition_values (device, [M]) receives the HVI of every candidate's
     UCB vector over the Pareto front of y_vector[:n_evaluations]; returns the global indices of
     the best batch_size candidates not equal to an evaluated point (select_next_batch's order)."""
     from .pareto import is_pareto_efficient
-    if batch_size > 16:
-        raise ValueError("hvi_select_indices handles batch_size <= 16")
+    if batch_size > _lib.MAX_TOPQ:
+        raise ValueError(f"hvi_select_indices handles batch_size <= {_lib.MAX_TOPQ}")
     y = y_vector[:n_evaluations]
     front = y[is_pareto_efficient(y)] if n_evaluations > 0 else np.zeros((0, len(reference_point)))
     if isinstance(front, torch.Tensor):

@@ -32,35 +32,54 @@ struct TopEntry {
   long long i;  // global candidate index, -1 = empty/excluded
 };
 
-__device__ __forceinline__ int bo_rank(double v, long long i) {
-  return i < 0 ? 0 : (v != v ? 2 : 1);
+// Branch-free order key: empty 0 < valid values (monotone in the value; -0.0 == 0.0) < NaN.
+__device__ __forceinline__ unsigned long long bo_order_key(double v, long long i) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v + 0.0);   // -0.0 -> +0.0
+  const unsigned long long m = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+  return i < 0 ? 0ull : (v != v ? ~0ull : m);
 }
 
-// strict "a comes before b" in the selection order
+// strict "a comes before b" in the selection order (selects only: the branchy three-way form
+// cost every comparison site a chain of exec-mask branches)
 __device__ __forceinline__ bool bo_better(double av, long long ai, double bv, long long bi) {
-  const int ra = bo_rank(av, ai), rb = bo_rank(bv, bi);
-  if (ra != rb) return ra > rb;
-  if (ra == 1 && av != bv) return av > bv;
-  if (ra == 0) return false;
-  return ai < bi;
+  const unsigned long long ka = bo_order_key(av, ai), kb = bo_order_key(bv, bi);
+  return ka > kb || (ka == kb && ka != 0ull && ai < bi);
 }
 
-// Sort the 64 (v, i) pairs held one per lane into selection order (lane 0 best):
-// bitonic network over __shfl_xor (64-wide wavefront).
+// "a comes before b" on precomputed order keys (bo_order_key) and indices
+__device__ __forceinline__ bool bo_key_before(unsigned long long ka, long long ia, unsigned long long kb,
+                                              long long ib) {
+  return ka > kb || (ka == kb && ka != 0ull && ia < ib);
+}
+
+// the value of an order key (empty -> -inf; NaN -> the canonical NaN; -0.0 comes back as +0.0)
+__device__ __forceinline__ double bo_key_value(unsigned long long k) {
+  const unsigned long long b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return k == 0ull ? -__builtin_inf() : (k == ~0ull ? __builtin_nan("") : __longlong_as_double((long long)b));
+}
+
+// Sort the 64 (v, i) pairs held one per lane into selection order (lane 0 best): bitonic
+// network over __shfl_xor (64-wide wavefront) on the order keys -- one key per element instead
+// of the three-way comparison per stage and direction (4x fewer instructions per stage).
 __device__ __forceinline__ void bo_wave_sort64(double& v, long long& i) {
   const int lane = threadIdx.x & 63;
+  unsigned long long k = bo_order_key(v, i);
+  long long x = i;
 #pragma unroll
-  for (int k = 2; k <= 64; k <<= 1) {
+  for (int k2 = 2; k2 <= 64; k2 <<= 1) {
 #pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const double pv = __shfl_xor(v, j, 64);
-      const long long pi = __shfl_xor(i, j, 64);
+    for (int j = k2 >> 1; j > 0; j >>= 1) {
+      const unsigned long long pk = __shfl_xor(k, j, 64);
+      const long long px = __shfl_xor(x, j, 64);
       const bool lower = (lane & j) == 0;
-      const bool desc = (lane & k) == 0;
-      const bool take = (lower == desc) ? bo_better(pv, pi, v, i) : bo_better(v, i, pv, pi);
-      if (take) { v = pv; i = pi; }
+      const bool desc = (lane & k2) == 0;
+      const bool take = (lower == desc) ? bo_key_before(pk, px, k, x) : bo_key_before(k, x, pk, px);
+      k = take ? pk : k;
+      x = take ? px : x;
     }
   }
+  v = bo_key_value(k);
+  i = x;
 }
 
 // Merge up to 16 new entries (held by lanes 0..15 as nv/ni) into the wave's running
@@ -85,6 +104,11 @@ __device__ __forceinline__ double bo_readlane_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)b, l);
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ unsigned long long bo_readlane_u(unsigned long long v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)v, l);
+  const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+  return ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
 }
 __device__ __forceinline__ long long bo_readlane_i(long long v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)v, l);
@@ -120,13 +144,15 @@ __device__ __forceinline__ void bo_wave_topq_insert16(double& lv, long long& li,
   const bool isL = lane < q;
   const double mv = isL ? lv : nv;
   const long long mi = isL ? li : ni;
+  // order keys computed once; the rounds broadcast keys and indices
+  const unsigned long long kn = bo_order_key(nv, ni), kl = bo_order_key(lv, li), km = isL ? kl : kn;
   int rank = isL ? lane : 0;
   for (unsigned long long m = nb; m; m &= m - 1) {
     const int s = __builtin_ctzll(m);
-    rank += bo_better(bo_readlane_d(nv, s), bo_readlane_i(ni, s), mv, mi) ? 1 : 0;
+    rank += bo_key_before(bo_readlane_u(kn, s), bo_readlane_i(ni, s), km, mi) ? 1 : 0;
   }
   for (int l = 0; l < q; ++l) {
-    const bool b = bo_better(bo_readlane_d(lv, l), bo_readlane_i(li, l), mv, mi);
+    const bool b = bo_key_before(bo_readlane_u(kl, l), bo_readlane_i(li, l), km, mi);
     rank += (beat && b) ? 1 : 0;
   }
   const bool keep = (isL || beat) && rank < q;
@@ -153,7 +179,10 @@ __device__ __forceinline__ void bo_wave_topq_insert16(double& lv, long long& li,
 // slots of the open-addressing tables).
 __host__ __device__ inline unsigned long long bo_point_key(const double* c, int dim) {
   unsigned long long h = 0x9E3779B97F4A7C15ull;
-  for (int k = 0; k < dim; ++k) {
+  // constant trip count (fully unrolled): a caller's coordinate array stays in registers
+#pragma unroll
+  for (int k = 0; k < BO_MAX_DIM; ++k) {
+    if (k >= dim) break;
     if (c[k] != c[k]) return 0ull;
     const double z = c[k] == 0.0 ? 0.0 : c[k];
     unsigned long long b;
@@ -184,7 +213,8 @@ __device__ __forceinline__ bool bo_hash_contains(const unsigned long long* keys,
     if (kt == key) {
       const double* r = pts + (long long)idx[t] * ld;
       bool eq = true;
-      for (int k = 0; k < dim; ++k) eq = eq && (r[k] == c[k]);
+#pragma unroll
+      for (int k = 0; k < BO_MAX_DIM; ++k) eq = eq && (k >= dim || r[k] == c[k]);
       if (eq) return true;
     }
   }
@@ -221,71 +251,82 @@ __device__ __forceinline__ TopEntry bo_block_best(double v, long long i, TopEntr
 }
 
 // Final merge of n_lists sorted top-q lists ([n_lists][q], any q <= BO_MAX_TOPQ) into out_v /
-// out_i in selection order; one workgroup of 1024 threads.
-//   T = the best of the lists' q-th entries.  The list holding T has q entries not worse than
-//   T, so the global top-q lies in S = {valid entries not worse than T} -- normally a handful
-//   (about q .. 2q).  S is compacted into LDS and each entry's rank in S (the number of S
-//   entries before it) is counted directly; rank r < q goes to slot r.  When |S| > 64 (mass
-//   ties, or fewer than q valid entries in total) q rounds of a workgroup arg-best over S, each
-//   retiring its winner by the strict order, finish instead.  Loads are batched 8 deep per
-//   thread.  (Round 1's q rounds of arg-best over every entry: 14 us at C2; an in-kernel
-//   last-workgroup merge measured slower still: its device-scope release fence and serial
-//   chain cost ~25 us at the end of the fused kernel.)
-static __global__ __launch_bounds__(1024) void bo_topq_merge_kernel(const TopEntry* __restrict__ L,
+// out_i in selection order; one workgroup of 256 threads (1024 measured slower: every wave sorts).
+//   T: every thread takes the best head of its lists, every wave sorts its 64 maxima (bitonic)
+//   and takes the q-th, T is the best of those -- q list heads (valid entries) are not worse
+//   than T, so the global top-q lies in S = {entries not worse than T}.  Only lists whose head is
+//   not worse than T contribute (normally about q of them); their entries not worse than T are
+//   compacted into LDS and each one's rank in S (the number of S entries before it) is counted;
+//   rank r < q goes to slot r.  Fallback when S exceeds the LDS (mass ties, or T empty because
+//   fewer than q entries exist and S is large): q rounds of a workgroup arg-best over every entry.
+// (The previous T -- the best of the lists' q-th entries -- left thousands of entries in S once
+// the lists came from blocks of thousands of candidates: 19 us at q = 3, 150 us at q = 16 and
+// 900 us at q = 48 for 512 lists, nearly all in the fallback.)
+#define BO_MERGE_CAP 1024
+static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntry* __restrict__ L,
                                                                     long long n_lists, int q,
                                                                     double* __restrict__ out_v,
                                                                     long long* __restrict__ out_i) {
   __shared__ TopEntry s_red[16];
-  __shared__ TopEntry s_buf[64];
-  __shared__ int s_cnt;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  if (tid == 0) s_cnt = 0;
+  __shared__ TopEntry s_buf[BO_MERGE_CAP];
+  __shared__ int s_lists[BO_MERGE_CAP];
+  __shared__ int s_cnt, s_nl;
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) { s_cnt = 0; s_nl = 0; }
   double bv = -__builtin_inf();
   long long bi = -1;
-  for (long long l0 = tid; l0 < n_lists; l0 += 8 * nt) {
-    TopEntry e[8];
+  for (long long l0 = tid; l0 < n_lists; l0 += 4 * nt) {
+    TopEntry e[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 4; ++u) {
       const long long l = l0 + (long long)u * nt;
-      e[u] = l < n_lists ? L[l * q + q - 1] : TopEntry{-__builtin_inf(), -1};
+      e[u] = l < n_lists ? L[l * q] : TopEntry{-__builtin_inf(), -1};
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < 4; ++u)
       if (bo_better(e[u].v, e[u].i, bv, bi)) { bv = e[u].v; bi = e[u].i; }
   }
-  const TopEntry T = bo_block_best(bv, bi, s_red);
-  const long long total = n_lists * q;
-  for (long long k0 = tid; k0 < total; k0 += 8 * nt) {
-    TopEntry e[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const long long k = k0 + (long long)u * nt;
-      e[u] = k < total ? L[k] : TopEntry{-__builtin_inf(), -1};
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (e[u].i >= 0 && !bo_better(T.v, T.i, e[u].v, e[u].i)) {
-        const int p = atomicAdd(&s_cnt, 1);
-        if (p < 64) s_buf[p] = e[u];
-      }
+  bo_wave_sort64(bv, bi);
+  {
+    const double wv = bo_readlane_d(bv, q - 1);
+    const long long wi = bo_readlane_i(bi, q - 1);
+    if (lane == 0) { s_red[wave].v = wv; s_red[wave].i = wi; }
+  }
+  __syncthreads();
+  TopEntry T = s_red[0];
+  for (int w = 1; w < (nt >> 6); ++w)
+    if (bo_better(s_red[w].v, s_red[w].i, T.v, T.i)) T = s_red[w];
+  for (long long l = tid; l < n_lists; l += nt) {
+    const TopEntry e = L[l * q];
+    if (e.i >= 0 && !bo_better(T.v, T.i, e.v, e.i)) {
+      const int p = atomicAdd(&s_nl, 1);
+      if (p < BO_MERGE_CAP) s_lists[p] = (int)l;
     }
   }
   __syncthreads();
-  const int cnt = s_cnt;
-  if (cnt <= 64) {
-    if (tid < 64) {
-      if (tid < cnt) {
-        const TopEntry me = s_buf[tid];
+  const int nl = s_nl;
+  if (nl <= BO_MERGE_CAP) {
+    for (int k = tid; k < nl * q; k += nt) {
+      const TopEntry e = L[(long long)s_lists[k / q] * q + k % q];
+      if (e.i >= 0 && !bo_better(T.v, T.i, e.v, e.i)) {
+        const int p = atomicAdd(&s_cnt, 1);
+        if (p < BO_MERGE_CAP) s_buf[p] = e;
+      }
+    }
+    __syncthreads();
+    const int cnt = s_cnt;
+    if (cnt <= BO_MERGE_CAP) {
+      for (int k = tid; k < cnt; k += nt) {
+        const TopEntry me = s_buf[k];
         int rank = 0;
         for (int m = 0; m < cnt; ++m) rank += bo_better(s_buf[m].v, s_buf[m].i, me.v, me.i) ? 1 : 0;
         if (rank < q) { out_v[rank] = me.v; out_i[rank] = me.i; }
-      } else if (tid < q) {
-        out_v[tid] = -__builtin_inf();
-        out_i[tid] = -1;
       }
+      for (int t = cnt + tid; t < q; t += nt) { out_v[t] = -__builtin_inf(); out_i[t] = -1; }
+      return;
     }
-    return;
   }
+  const long long total = n_lists * q;
   double pv = 0.0;
   long long pi = -1;                                 // previous winner (none yet)
   for (int r = 0; r < q; ++r) {

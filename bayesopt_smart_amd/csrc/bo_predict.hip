@@ -759,7 +759,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   if (e != hipSuccess) return BO_ERR_HIP;
   if (timed) timer_mark(s);
   if (d->topq > 0) {
-    hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(1024), 0, s, partial,
+    hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(256), 0, s, partial,
                        (long long)pl.grid * pl.waves, d->topq, d->top_val, (long long*)d->top_idx);
     BO_CHECK_HIP(hipGetLastError());
   }

@@ -107,7 +107,7 @@ struct SelArgs {
   long long grid_lo[BO_MAX_DIM], grid_shape[BO_MAX_DIM];
   const double* excl;
   // open-addressing hash set of the evaluated points (keys: bo_point_key, 0 = empty; idx: the
-  // point's row): built per workgroup in LDS (lds_slots > 0, select_lane_kernel), else in the
+  // point's row): built per workgroup in LDS (lds_slots > 0), else in the
   // workspace (hkeys), else NULL (the exclusion scans the points)
   int lds_slots;
   const unsigned long long* hkeys;
@@ -133,11 +133,25 @@ __device__ __forceinline__ bool cand_excluded(const SelArgs& a, long long j,
                                               const unsigned long long* hk, const int* hi,
                                               unsigned int hm) {
   double c[BO_MAX_DIM];
-  for (int k = 0; k < a.dim; ++k) c[k] = cand_coord(a, j, k);
+  if (a.kind == BO_CAND_GRID) {          // all coordinates from one chain of divisions
+    long long gi = a.cand_offset + j;
+#pragma unroll
+    for (int k = BO_MAX_DIM - 1; k >= 0; --k) {
+      c[k] = 0.0;
+      if (k < a.dim) {
+        c[k] = (double)(a.grid_lo[k] + gi % a.grid_shape[k]);
+        gi /= a.grid_shape[k];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < BO_MAX_DIM; ++k) c[k] = k < a.dim ? cand_coord(a, j, k) : 0.0;
+  }
   if (hk) return bo_hash_contains(hk, hi, hm, a.excl, a.dim, c, a.dim);
   for (int e = 0; e < a.n_excl; ++e) {
     bool eq = true;
-    for (int k = 0; k < a.dim; ++k) eq = eq && (a.excl[(long long)e * a.dim + k] == c[k]);
+#pragma unroll
+    for (int k = 0; k < BO_MAX_DIM; ++k) eq = eq && (k >= a.dim || a.excl[(long long)e * a.dim + k] == c[k]);
     if (eq) return true;
   }
   return false;
@@ -152,57 +166,26 @@ __device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int 
   return (double)(a.grid_lo[k] + gi % a.grid_shape[k]);
 }
 
-// grid-stride over candidates; each wave folds 64 candidates per step into its running
-// top-q (4 inserts of 16), then writes its list to `partial`.
-__global__ __launch_bounds__(256) void select_kernel(SelArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double lv = -__builtin_inf();
-  long long li = -1;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long base = (long long)blockIdx.x * blockDim.x + wave * 64; base < a.n_cand;
-       base += stride) {
-    const long long j = base + lane;
-    double v = -__builtin_inf();
-    long long gi = -1;
-    if (j < a.n_cand) {
-      v = a.acq[j];
-      gi = a.cand_offset + j;
-    }
-    // the O(n_excl) exclusion test only for candidates that beat the wave's current q-th entry
-    // (the others cannot enter the list whether excluded or not); after the first steps of the
-    // grid-stride almost no wave-step needs it
-    const double tv = __shfl(lv, a.topq - 1, 64);
-    const long long ti = __shfl(li, a.topq - 1, 64);
-    const bool need = a.n_excl > 0 && gi >= 0 && bo_better(v, gi, tv, ti);
-    if (__ballot(need) != 0ull && need) {
-      if (cand_excluded(a, j, a.hkeys, a.hidx, a.hmask)) gi = -1;
-    }
-#pragma unroll
-    for (int grp = 0; grp < 4; ++grp) {
-      const double nv = __shfl(v, (lane & 15) + 16 * grp, 64);
-      const long long ni = __shfl(gi, (lane & 15) + 16 * grp, 64);
-      bo_wave_topq_insert(lv, li, nv, ni, a.topq);
-    }
-  }
-  if (lane < a.topq) {
-    TopEntry* dst = a.partial + ((size_t)blockIdx.x * 4 + wave) * a.topq;
-    dst[lane].v = lv;
-    dst[lane].i = li;
-  }
-}
-
 // ---------------------------------------------------------------------------------------
-// Selection for q <= 16 (every batch the reference's demos use), ONE pass at HBM rate:
-// every thread keeps its own sorted top-Q (Q = 8 / 16 / 24, at least q + 4) in registers over
-// a coalesced grid-stride sweep -- almost every element is rejected by one comparison with the
-// thread's Q-th entry.  The exclusion of evaluated points is deferred to the Q list entries of
-// each thread (hash set of the points, built in LDS by every workgroup), so the sweep reads
-// nothing but the acquisition values.  Then the wave (wave_lists_topq: threshold set + ranks)
-// and the workgroup (ranks of the 4 wave lists) reduce the lists to the workgroup's top-q, and
-// bo_topq_merge_kernel merges those.
-// M > 0 fuses the exact hypervolume improvement of bo_hvi.hip into the sweep: the acquisition
-// of candidate i is computed from its M UCB values and the boxes (wave-uniform, scalar loads),
-// written to acq, and selected in the same pass (one HBM read of the UCB arrays in total).
+// select_next_batch (acquisition.py:116-144) over a stored acquisition array -- or, M >= 1,
+// over the exact hypervolume improvement computed from the UCB arrays in the same pass (the
+// HVI of bo_hvi.hip, written to acq as it is computed).  One HBM pass at stream rate, any
+// q <= BO_MAX_TOPQ.  Each wave keeps its running top-q sorted in lanes 0..q-1 and the list's
+// q-th entry T wave-uniform; the sweep loads U elements per lane and looks again only at the
+// elements not below T (one compare per element; NaN passes).  When some element beats T (an
+// "event": every batch of a wave's first step, rarely later):
+//  * more than 64 such elements: the q-th best of the lanes' best ones (bitonic over 64 lanes)
+//    bounds them -- q elements are not worse than it -- and only the elements not worse than
+//    the bound are taken (normally q .. 2q); the rest stay pending and are taken in a second
+//    round only if they still beat the updated T (when the bound's q elements included
+//    evaluated points);
+//  * the taken elements are compacted into LDS, 64 at a time one per lane, tested against the
+//    evaluated points (hash set, built in LDS by every workgroup, else in the workspace) and
+//    inserted by ranks (wave_rank_insert; the first insert of a wave sorts instead).
+// Every wave writes its list to `partial` ([blocks * 4][q]); bo_topq_merge_kernel merges them.
+// The first round-2 version kept a sorted top-Q per thread (Q = 8/16/24 >= q + 4, exclusion
+// deferred to the list entries): 100-300 KB of unrolled code per instantiation and up to 400
+// VGPRs (scratch at Q = 24) -- 38 us at C3 and 1.9 ms at C5 (q = 16) for 8 / 32 MB.
 // ---------------------------------------------------------------------------------------
 struct HviIn {
   const double* ucb;          // [M][ld]
@@ -213,114 +196,48 @@ struct HviIn {
   double* acq_out;
 };
 
-template <int Q>
-__device__ __forceinline__ void lane_insert(double (&v)[Q], long long (&ix)[Q], double nv, long long ni) {
-  // sorted best-first; nv beats v[Q - 1] (checked by the caller)
-#pragma unroll
-  for (int k = Q - 1; k >= 0; --k) {
-    const bool beats_k = bo_better(nv, ni, v[k], ix[k]);
-    const bool beats_prev = k > 0 && bo_better(nv, ni, v[k > 0 ? k - 1 : 0], ix[k > 0 ? k - 1 : 0]);
-    if (beats_k) {
-      v[k] = beats_prev ? v[k - (k > 0)] : nv;
-      ix[k] = beats_prev ? ix[k - (k > 0)] : ni;
-    }
-  }
+// LDS written by some lanes of a wave and read back by others: keep the compiler's order (the
+// LDS executes one wave's operations in issue order).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The top-q (q <= Q) of a wave's per-lane sorted lists, into out[0..q-1] (LDS):
-//   T = the best of the lanes' q-th entries; S = the entries not worse than T -- a prefix of
-//   every lane's list, normally about q .. 2q entries -- compacted into buf (64 entries, LDS)
-//   by one ballot per list slot, each ranked by a scan of S.  |S| > 64 (fewer than q valid
-//   entries per lane, or mass ties): q rounds of a wave arg-best, the owner popping its head.
-// (Round 1 ran Q arg-best rounds at the wave and again at the workgroup level: 6 shuffle
-// stages of (value, index) pairs per round.)  Called by all waves of the workgroup together.
-constexpr int BO_SEL_Q = 16;
-// `excluded(idx)` tests a list entry (global index) against the evaluated points; `purge()`
-// drops every excluded entry of the calling lane's list (and rebuilds the list if too few
-// remain).  The exclusion is only tested on S: when no entry of S is excluded, S also holds the
-// top-q of the non-excluded elements; otherwise (rare) every lane purges and T, S are redone.
-template <int Q, class Excl, class Purge>
-__device__ __forceinline__ void wave_lists_topq(double (&v)[Q], long long (&ix)[Q], int q,
-                                                TopEntry* buf, TopEntry* out, bool check,
-                                                Excl excluded, Purge purge) {
+// Insert the entries (nv, ni) of the lanes with `pass` into the wave's list (sorted in lanes
+// 0..q-1, q <= 64; empty entries have i = -1).  Every list entry and every new entry counts the
+// entries before it in selection order -- its rank in the union: list entries know their own
+// position and compare with the new ones, new entries compare with both (v_readlane broadcasts,
+// |new| + q rounds) -- and ranks < q are written to LDS slot `rank` of this wave's `buf`.
+__device__ __forceinline__ void wave_rank_insert(double& lv, long long& li, double nv, long long ni,
+                                                 bool pass, int q, TopEntry* buf) {
   const int lane = threadIdx.x & 63;
-  double bv;
-  long long bi;
-  int c;
-  for (;;) {
-    bv = -__builtin_inf();
-    bi = -1;
-#pragma unroll
-    for (int k = 0; k < Q; ++k)
-      if (k == q - 1) { bv = v[k]; bi = ix[k]; }
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) {
-      const double ov = __shfl_xor(bv, m, 64);
-      const long long oi = __shfl_xor(bi, m, 64);
-      if (bo_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-    }
-    c = 0;                                            // length of this lane's prefix in S
-#pragma unroll
-    for (int k = 0; k < Q; ++k)
-      if (k < q && ix[k] >= 0 && !bo_better(bv, bi, v[k], ix[k])) c = k + 1;
-    if (!check) break;
-    bool bad = false;
-#pragma unroll
-    for (int k = 0; k < Q; ++k)
-      if (k < c) bad = bad || excluded(ix[k]);
-    if (__ballot(bad) == 0ull) break;
-    purge();
-    check = false;
+  const unsigned long long nb = __ballot(pass);
+  if (nb == 0ull) return;
+  const unsigned long long kn = bo_order_key(nv, ni), kl = bo_order_key(lv, li);
+  int rl = lane, rn = 0;
+  for (unsigned long long m = nb; m; m &= m - 1) {
+    const int s = __builtin_ctzll(m);
+    const unsigned long long sk = bo_readlane_u(kn, s);
+    const long long si = bo_readlane_i(ni, s);
+    rn += bo_key_before(sk, si, kn, ni) ? 1 : 0;
+    rl += bo_key_before(sk, si, kl, li) ? 1 : 0;
   }
-  int total = 0;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int k = 0; k < Q; ++k) {
-    if (k >= q) break;
-    const unsigned long long b = __ballot(c > k);
-    const int off = total + __popcll(b & lt);
-    if (c > k && off < 64) { buf[off].v = v[k]; buf[off].i = ix[k]; }
-    total += __popcll(b);
-  }
-  __syncthreads();
-  if (total <= 64) {
-    if (lane < total) {
-      const TopEntry me = buf[lane];
-      int rank = 0;
-      for (int m = 0; m < total; ++m) rank += bo_better(buf[m].v, buf[m].i, me.v, me.i) ? 1 : 0;
-      if (rank < q) out[rank] = me;
-    } else if (lane < q) {
-      out[lane].v = -__builtin_inf();
-      out[lane].i = -1;
-    }
-    return;
-  }
-#pragma unroll 1
-  for (int r = 0; r < q; ++r) {
-    double hv = v[0];
-    long long hi = ix[0];
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) {
-      const double ov = __shfl_xor(hv, m, 64);
-      const long long oi = __shfl_xor(hi, m, 64);
-      if (bo_better(ov, oi, hv, hi)) { hv = ov; hi = oi; }
-    }
-    if (lane == 0) { out[r].v = hv; out[r].i = hi; }
-    if (hi >= 0 && ix[0] == hi) {
-#pragma unroll
-      for (int k = 0; k + 1 < Q; ++k) { v[k] = v[k + 1]; ix[k] = ix[k + 1]; }
-      v[Q - 1] = -__builtin_inf();
-      ix[Q - 1] = -1;
-    }
-  }
+  for (int l = 0; l < q; ++l)
+    rn += bo_key_before(bo_readlane_u(kl, l), bo_readlane_i(li, l), kn, ni) ? 1 : 0;
+  wave_lds_sync();
+  if (lane < q && rl < q) { buf[rl].v = lv; buf[rl].i = li; }
+  if (pass && rn < q) { buf[rn].v = nv; buf[rn].i = ni; }
+  wave_lds_sync();
+  if (lane < q) { lv = buf[lane].v; li = buf[lane].i; }
 }
 
-template <int Q, int M>
-__global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
+template <int M, int U>
+__global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lkeys[];   // [lds_slots], then idx
-  __shared__ TopEntry wl[4 * BO_SEL_Q];
-  __shared__ TopEntry wbuf[4 * 64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ TopEntry wbuf[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = a.topq;
+  TopEntry* buf = wbuf[wave];
   // the evaluated points' hash set, in LDS when small (built by every workgroup: no extra
   // launches), else the workspace table, else none (scan)
   const unsigned long long* hk = a.hkeys;
@@ -339,118 +256,134 @@ __global__ __launch_bounds__(256) void select_lane_kernel(SelArgs a, HviIn h) {
     hi = lidx;
     hm = (unsigned int)a.lds_slots - 1;
   }
-  double v[Q];
-  long long ix[Q];
+  double lv = -__builtin_inf(), tv = -__builtin_inf();   // list entry; the list's q-th (uniform)
+  long long li = -1, ti = -1;
+  const unsigned long long below = (1ull << lane) - 1ull;
   const long long stride = (long long)gridDim.x * blockDim.x;
-  // U elements per thread and sweep step, all loaded before any is processed (the loads of a
-  // step are in flight together; the loop body alone would expose one latency per element).
-  // The sweep itself ignores the exclusion (check = false): see below.
-  constexpr int U = 4;
-  auto sweep = [&](bool check) {
+  // wave-uniform trip count: every lane stays in the loop for the ballots and broadcasts
+  for (long long b0 = (long long)blockIdx.x * blockDim.x + wave * 64; b0 < a.n_cand; b0 += U * stride) {
+    double val[U];
+    bool any = false;
 #pragma unroll
-    for (int k = 0; k < Q; ++k) { v[k] = -__builtin_inf(); ix[k] = -1; }
-    for (long long j0 = (long long)blockIdx.x * blockDim.x + tid; j0 < a.n_cand; j0 += U * stride) {
-      double val[U];
+    for (int u = 0; u < U; ++u) {     // all U loads in flight before any element is looked at
+      const long long j = b0 + u * stride + lane;
+      const bool in = j < a.n_cand;
+      if constexpr (M == 0) {
+        val[u] = in ? a.acq[j] : 0.0;
+      } else {
+        double p[M];
+        bool nan = false;
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long long j = j0 + u * stride;
-        const bool in = j < a.n_cand;
-        if constexpr (M == 0) {
-          val[u] = in ? a.acq[j] : 0.0;
-        } else {
-          double p[M];
-          bool nan = false;
+        for (int k = 0; k < M; ++k) {
+          p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
+          nan = nan || (p[k] != p[k]);
+        }
+        double hv = 0.0;
+        const double* b = h.boxes;
+        for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
+          double w = 1.0;
 #pragma unroll
           for (int k = 0; k < M; ++k) {
-            p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
-            nan = nan || (p[k] != p[k]);
+            const double hi2 = p[k] < b[M + k] ? p[k] : b[M + k];
+            w *= fmax(hi2 - b[k], 0.0);
           }
-          double hv = 0.0;
-          const double* b = h.boxes;
-          for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
-            double w = 1.0;
-#pragma unroll
-            for (int k = 0; k < M; ++k) {
-              const double hi2 = p[k] < b[M + k] ? p[k] : b[M + k];
-              w *= fmax(hi2 - b[k], 0.0);
-            }
-            hv += w;
-          }
-          val[u] = nan ? __builtin_nan("") : hv;
-          if (in) h.acq_out[j] = val[u];
+          hv += w;
         }
+        val[u] = nan ? __builtin_nan("") : hv;
+        if (in) h.acq_out[j] = val[u];
       }
+      any = any || (in && !(val[u] < tv));
+    }
+    if (__ballot(any) == 0ull) continue;
+    // ---- event: the elements beating T (exact order) are pending
+    bool pend[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long j = b0 + u * stride + lane;
+      pend[u] = j < a.n_cand && bo_better(val[u], a.cand_offset + j, tv, ti);
+    }
+    for (;;) {
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) cnt += __popcll(__ballot(pend[u]));
+      if (cnt == 0) break;
+      double bv = -__builtin_inf();   // the bound (empty: take every pending element)
+      long long bix = -1;
+      if (cnt > 64) {
+        unsigned long long mk = 0ull;
+        long long mi = -1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long gi = a.cand_offset + b0 + u * stride + lane;
+          const unsigned long long k = pend[u] ? bo_order_key(val[u], gi) : 0ull;
+          const bool b = bo_key_before(k, gi, mk, mi);
+          mk = b ? k : mk;
+          mi = b ? gi : mi;
+        }
+        double mv = bo_key_value(mk);
+        bo_wave_sort64(mv, mi);
+        bv = bo_readlane_d(mv, q - 1);
+        bix = bo_readlane_i(mi, q - 1);
+      }
+      bool take[U];
+      int off[U], total = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long long j = j0 + u * stride;
-        if (j >= a.n_cand) break;
-        const long long gi = a.cand_offset + j;
-        if (!bo_better(val[u], gi, v[Q - 1], ix[Q - 1])) continue;
-        if (check && cand_excluded(a, j, hk, hi, hm)) continue;
-        lane_insert<Q>(v, ix, val[u], gi);
+        const long long gi = a.cand_offset + b0 + u * stride + lane;
+        take[u] = pend[u] && !bo_better(bv, bix, val[u], gi);
+        const unsigned long long bb = __ballot(take[u]);
+        off[u] = total + __popcll(bb & below);
+        total += __popcll(bb);
       }
-    }
-  };
-  sweep(false);
-  // Deferred exclusion (acquisition.py:137-139): tested on the wave's threshold set S only
-  // (wave_lists_topq); purge() runs when an entry of S is an evaluated point.  Without its
-  // excluded entries a list still holds its thread's best non-excluded elements; it needs q of
-  // them unless it held every element of the thread (Q - q >= 4), else the thread rescans with
-  // per-element tests.
-  auto excluded = [&](long long gi) { return gi >= 0 && cand_excluded(a, gi - a.cand_offset, hk, hi, hm); };
-  auto purge = [&]() {
-    const bool full = ix[Q - 1] >= 0;
-    bool ex[Q];
-    int removed = 0;
+#pragma unroll 1
+      for (int c0 = 0; c0 < total; c0 += 64) {
+        wave_lds_sync();
 #pragma unroll
-    for (int k = 0; k < Q; ++k) {
-      ex[k] = excluded(ix[k]);
-      removed += ex[k] ? 1 : 0;
-    }
-    if (removed == 0) return;
-    if (full && Q - removed < a.topq) {
-      sweep(true);
-      return;
-    }
-#pragma unroll
-    for (int k = Q - 1; k >= 0; --k) {
-      if (ex[k]) {
-#pragma unroll
-        for (int t = k; t + 1 < Q; ++t) { v[t] = v[t + 1]; ix[t] = ix[t + 1]; }
-        v[Q - 1] = -__builtin_inf();
-        ix[Q - 1] = -1;
-      }
-    }
-  };
-  // wave, then workgroup: the top-q of the lanes' lists (wave_lists_topq), then of the 4 wave
-  // lists (rank by LDS scan); the workgroup's list goes to `partial` ([blocks][q])
-  wave_lists_topq<Q>(v, ix, a.topq, wbuf + wave * 64, wl + wave * BO_SEL_Q, a.n_excl > 0,
-                     excluded, purge);
-  __syncthreads();
-  if (wave == 0) {
-    const int n = 4 * a.topq;
-    TopEntry* dst = a.partial + (size_t)blockIdx.x * a.topq;
-    if (lane < a.topq) { dst[lane].v = -__builtin_inf(); dst[lane].i = -1; }
-    if (lane < n) {
-      const TopEntry me = wl[(lane / a.topq) * BO_SEL_Q + lane % a.topq];
-      if (me.i >= 0) {
-        int rank = 0;
-        for (int m = 0; m < n; ++m) {
-          const TopEntry o = wl[(m / a.topq) * BO_SEL_Q + m % a.topq];
-          rank += bo_better(o.v, o.i, me.v, me.i) ? 1 : 0;
+        for (int u = 0; u < U; ++u)
+          if (take[u] && off[u] >= c0 && off[u] < c0 + 64) {
+            buf[off[u] - c0].v = val[u];
+            buf[off[u] - c0].i = a.cand_offset + b0 + u * stride + lane;
+          }
+        wave_lds_sync();
+        bool p = lane < total - c0;
+        const double nv = p ? buf[lane].v : -__builtin_inf();
+        const long long ni = p ? buf[lane].i : -1;
+        p = p && bo_better(nv, ni, tv, ti);
+        if (a.n_excl > 0 && p) p = !cand_excluded(a, ni - a.cand_offset, hk, hi, hm);
+        if (__ballot(p) == 0ull) continue;
+        if (bo_readlane_i(li, 0) < 0 && __popcll(__ballot(p)) > 24) {
+          // empty list and a large chunk: the sorted chunk's head is the list (rank insertion
+          // costs |chunk| + q broadcast rounds)
+          double sv = p ? nv : -__builtin_inf();
+          long long si = p ? ni : -1;
+          bo_wave_sort64(sv, si);
+          lv = lane < q ? sv : -__builtin_inf();
+          li = lane < q ? si : -1;
+        } else {
+          wave_rank_insert(lv, li, nv, ni, p, q, buf);
         }
-        if (rank < a.topq) dst[rank] = me;
+        tv = bo_readlane_d(lv, q - 1);
+        ti = bo_readlane_i(li, q - 1);
+      }
+      // what the bound held back stays pending only while it still beats T
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long gi = a.cand_offset + b0 + u * stride + lane;
+        pend[u] = pend[u] && !take[u] && bo_better(val[u], gi, tv, ti);
       }
     }
+  }
+  if (lane < q) {
+    TopEntry* dst = a.partial + ((size_t)blockIdx.x * 4 + wave) * q;
+    dst[lane].v = lv;
+    dst[lane].i = li;
   }
 }
 
 template <int M>
-int launch_select_lane(const SelArgs& a, const HviIn& h, int q, int blocks, hipStream_t s) {
+int launch_select_stream(const SelArgs& a, const HviIn& h, int blocks, hipStream_t s) {
   const size_t lds = (size_t)a.lds_slots * 12;
-  if (q <= 4) hipLaunchKernelGGL((select_lane_kernel<8, M>), dim3(blocks), dim3(256), lds, s, a, h);
-  else if (q <= 12) hipLaunchKernelGGL((select_lane_kernel<16, M>), dim3(blocks), dim3(256), lds, s, a, h);
-  else hipLaunchKernelGGL((select_lane_kernel<24, M>), dim3(blocks), dim3(256), lds, s, a, h);
+  hipLaunchKernelGGL((select_stream_kernel<M, M == 0 ? 8 : 4>), dim3(blocks), dim3(256), lds, s, a, h);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
 }
@@ -489,7 +422,7 @@ __global__ __launch_bounds__(256) void pareto_kernel(const double* __restrict__ 
   if (i < n) mask[i] = dominated ? 0 : 1;
 }
 
-// partial lists: bitonic path <= 1024 workgroups x 4 waves x q; lane path <= 8192 entries
+// partial lists: <= 1024 workgroups x 4 waves x q entries
 size_t sel_lists_bytes(int topq) {
   const size_t e = (size_t)1024 * 4 * (topq > 0 ? topq : 1);
   return (e > 8192 ? e : 8192) * sizeof(TopEntry);
@@ -637,12 +570,12 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   a.excl = excl;
   a.partial = (TopEntry*)ws;
   if (n_excl > 0 && n_cand > 0) {
-    // the evaluated points' hash set: per workgroup in LDS (<= 1024 points, one-pass kernel),
+    // the evaluated points' hash set: per workgroup in LDS (<= 1024 points),
     // else in the workspace region after the lists when it fits (2 n_excl .. 4 n_excl slots of
     // 12 B), else none (the exclusion scans the points)
     const unsigned int slots = bo_hash_slots(n_excl);
     const size_t region = ((size_t)n_cand + 31) / 32 * 4;
-    if (topq <= 16 && n_excl <= 1024) {
+    if (n_excl <= 1024) {
       a.lds_slots = (int)slots;
     } else if ((size_t)slots * 12 <= region) {
       unsigned long long* keys = (unsigned long long*)((char*)ws + sel_lists_bytes(topq));
@@ -656,39 +589,27 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
       a.hmask = slots - 1;
     }
   }
-  long long blocks = (n_cand + 255) / 256;
-  if (topq <= 16) {
-    // two workgroups per CU (8 per CU measured slower: the per-workgroup list merges and the
-    // longer final merge outweigh the extra loads in flight); blocks x Q <= 8192 list entries
-    const int max_blocks = 2 * cus_count() < 512 ? 2 * cus_count() : 512;
-    if (blocks > max_blocks) blocks = max_blocks;
-    if (blocks < 1) blocks = 1;
-    HviIn hz;
-    memset(&hz, 0, sizeof(hz));
-    const HviIn& hv = h ? *h : hz;
-    int st;
-    switch (m) {
-      case 0: st = launch_select_lane<0>(a, hv, topq, (int)blocks, s); break;
-      case 1: st = launch_select_lane<1>(a, hv, topq, (int)blocks, s); break;
-      case 2: st = launch_select_lane<2>(a, hv, topq, (int)blocks, s); break;
-      case 3: st = launch_select_lane<3>(a, hv, topq, (int)blocks, s); break;
-      case 4: st = launch_select_lane<4>(a, hv, topq, (int)blocks, s); break;
-      default: return BO_ERR_UNSUPPORTED;
-    }
-    if (st != BO_OK) return st;
-    hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
-                       blocks, topq, top_val, (long long*)top_idx);
-    BO_CHECK_HIP(hipGetLastError());
-    return BO_OK;
-  }
-  if (m != 0) return BO_ERR_UNSUPPORTED;   // (the caller runs the HVI scan first for q > 16)
-  // q > 16: per-wave bitonic lists, one workgroup per CU
-  const int max_blocks = cus_count() < 1024 ? cus_count() : 1024;
+  // U = 8 elements per thread and step (M == 0): one workgroup per 2048 elements, at most 4 per
+  // CU (16 waves; the whole C3 array in flight at once); [blocks * 4][q] lists for the merge
+  const long long per_block = 256LL * (m == 0 ? 8 : 4);
+  long long blocks = (n_cand + per_block - 1) / per_block;
+  const int max_blocks = 4 * cus_count() < 1024 ? 4 * cus_count() : 1024;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(select_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
-  BO_CHECK_HIP(hipGetLastError());
-  hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(1024), 0, s, (const TopEntry*)ws,
+  HviIn hz;
+  memset(&hz, 0, sizeof(hz));
+  const HviIn& hv = h ? *h : hz;
+  int st;
+  switch (m) {
+    case 0: st = launch_select_stream<0>(a, hv, (int)blocks, s); break;
+    case 1: st = launch_select_stream<1>(a, hv, (int)blocks, s); break;
+    case 2: st = launch_select_stream<2>(a, hv, (int)blocks, s); break;
+    case 3: st = launch_select_stream<3>(a, hv, (int)blocks, s); break;
+    case 4: st = launch_select_stream<4>(a, hv, (int)blocks, s); break;
+    default: return BO_ERR_UNSUPPORTED;
+  }
+  if (st != BO_OK) return st;
+  hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(256), 0, s, (const TopEntry*)ws,
                      blocks * 4, topq, top_val, (long long*)top_idx);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
@@ -716,13 +637,6 @@ int bo_hvi_select_topq(double* acq, const double* ucb, int64_t ld, int64_t n_can
       (n_boxes > 0 && !boxes))
     return BO_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (topq > 16) {   // large batches: the standalone HVI scan, then the bitonic selection
-    const int st = bo_hypervolume_improvement_exact(acq, ucb, ld, n_cand, n_obj, shift, scale, boxes,
-                                                    n_boxes, stream);
-    if (st != BO_OK) return st;
-    return select_impl(acq, n_cand, kind, cand, grid_lo, grid_shape, dim, cand_offset, excl, n_excl,
-                       topq, top_val, top_idx, ws, ws_bytes, s, nullptr, 0);
-  }
   HviIn h;
   memset(&h, 0, sizeof(h));
   h.ucb = ucb;

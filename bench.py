@@ -568,8 +568,8 @@ def main():
 
 def standalone_select(lib, bo, acq, cands, offset, n, xd, q, dev, fused_sel, reps=20):
     """bo_select_topq (select_next_batch over a stored acquisition array, acquisition.py:116-144)
-    on this shard's acq array from the timed run, with the evaluated points excluded: HIP-event
-    time per call (one-pass selection kernel + the final merge), its HBM rate on the 8 B per
+    on this shard's acq array from the timed run, with the evaluated points excluded: device time
+    per call (one-pass selection kernel + the final merge, HIP-graph replayed), its HBM rate on the 8 B per
     candidate it must read, and whether it selects what the fused kernel selected.  Outside the
     timed region."""
     import ctypes
@@ -580,23 +580,33 @@ def standalone_select(lib, bo, acq, cands, offset, n, xd, q, dev, fused_sel, rep
     glo = (ctypes.c_int64 * 8)(*((list(cands.lo) if cands.lo else []) + [0] * (8 - len(cands.lo or []))))
     gsh = (ctypes.c_int64 * 8)(*((list(cands.shape) if cands.shape else []) + [1] * (8 - len(cands.shape or []))))
     carg = cands.tensor[offset:].data_ptr() if cands.kind in ("i64", "f64") else cands.cand_arg
-    strm = bo.device.stream_handle(dev)
 
-    def call():
+    def call(strm):
         bo._lib.check(lib.bo_select_topq(acq.data_ptr(), n, cands.kind_code, carg, glo, gsh, cands.dim,
                                          offset, xd.data_ptr(), xd.shape[0], q, tv.data_ptr(),
                                          ti.data_ptr(), ws.data_ptr(), ws.numel(), strm), "select")
-    call()
+    call(bo.device.stream_handle(dev))
+    torch.cuda.synchronize()
+    got = ti.cpu().numpy()
+    # the reps calls replayed as one HIP graph: device time per call, no host launch cost
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        call(side.cuda_stream)
+        with torch.cuda.graph(g, stream=side):
+            for _ in range(reps):
+                call(side.cuda_stream)
+    torch.cuda.current_stream(dev).wait_stream(side)
+    g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(reps):
-        call()
+    g.replay()
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    got = ti.cpu().numpy()
-    return {"kernels": f"select_lane_kernel<{8 if q <= 4 else 16 if q <= 12 else 24}, 0> + bo_topq_merge_kernel",
+    return {"kernels": "select_stream_kernel<0, 8> + bo_topq_merge_kernel (HIP-graph replay)",
             "ms": ms, "bytes": 8 * n, "achieved_GBps": 8 * n / (ms * 1e-3) / 1e9,
             "hbm_frac": 8 * n / (ms * 1e-3) / 1e9 / 8000.0,
             "matches_fused_selection": bool(np.array_equal(got[got >= 0], np.asarray(fused_sel)))}

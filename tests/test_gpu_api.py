@@ -151,21 +151,20 @@ def test_select_next_batch_large_batch_and_exhaustion(bo):
 
 
 @pytest.mark.parametrize("kind", ["grid", "f64"])
-@pytest.mark.parametrize("q", [3, 8, 16])
-def test_select_deferred_exclusion_paths(bo, kind, q):
-    """bo_select_topq's one-pass kernel tests the exclusion only on each wave's threshold set:
-    here the best candidates of the whole set are evaluated points, all in the list of ONE
-    thread of the grid-stride sweep (its elements j = t + k * stride), so that set is purged
-    and that thread rescans with per-element tests; plus evaluated points scattered over the
-    top of the order.  Exact selection order against numpy."""
+@pytest.mark.parametrize("q", [3, 8, 16, 33, 48])
+def test_select_exclusion_at_the_top(bo, kind, q):
+    """bo_select_topq's streaming kernel tests the exclusion only for elements that beat their
+    wave's running q-th entry: here the best candidates of the whole set are evaluated points
+    (128 of them, every 2^14-th element, more than any q, so that many waves meet
+    several of them), plus evaluated points scattered over the top of the order.  Exact
+    selection order against numpy, every q up to BO_MAX_TOPQ."""
     import torch
     side0, side1 = 2048, 1024
     m = side0 * side1
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    stride = min((m + 255) // 256, 2 * cus, 512) * 256
+    stride = 1 << 14
     rng = np.random.default_rng(q)
     acq = rng.standard_normal(m)
-    hot = 7 + stride * np.arange(m // stride)              # thread 7's elements
+    hot = 7 + stride * np.arange(m // stride)
     acq[hot] = 100.0 + np.arange(hot.size)                  # the best of all, evaluated below
     lin = np.arange(m)
     cand_pts = np.stack([lin // side1, lin % side1], axis=1)

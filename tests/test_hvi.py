@@ -129,13 +129,13 @@ def test_device_hvi_full_scan_properties():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,m,q", [("grid", 2, 3), ("grid", 3, 16), ("f64", 2, 8), ("sobol", 3, 5),
-                                      ("grid", 2, 20)])
+                                      ("grid", 2, 20), ("sobol", 2, 48)])
 def test_fused_hvi_select_matches_scan_plus_oracle_select(kind, m, q):
     """bo_hvi_select_topq (exact HVI and its top-q in one pass) writes the same acquisition
     array as the standalone HVI scan, bit for bit, and selects what select_next_batch
     (acquisition.py:116-144, the oracle's deterministic order) selects over it, evaluated
-    points skipped (grid: bitmap; explicit / Sobol: exact coordinates).  q = 20 takes the
-    two-step path (scan, then the bitonic selection)."""
+    points skipped (hash set of the evaluated points, exact coordinates), for q up to
+    BO_MAX_TOPQ."""
     import torch
     from bayesopt_smart_amd.acquisition import hvi_select_indices, hypervolume_improvement_exact
     from bayesopt_smart_amd.predict import CandidateSet
@@ -154,14 +154,10 @@ def test_fused_hvi_select_matches_scan_plus_oracle_select(kind, m, q):
     ev = cands.points(rng.choice(n, 40, replace=False)).astype(np.float64)
     ref_pt = np.full(m, -4.0)
     acq = torch.zeros(n, dtype=torch.float64, device="cuda")
-    idx = hvi_select_indices(acq, ucb, y, 40, ref_pt, pm, pv, cands, ev, q) if q <= 16 else None
+    idx = hvi_select_indices(acq, ucb, y, 40, ref_pt, pm, pv, cands, ev, q)
     front = y[O.is_pareto_efficient(y)]
     scan = hypervolume_improvement_exact(ucb, front, ref_pt, pm, pv).cpu().numpy()
-    if q <= 16:
-        np.testing.assert_array_equal(acq.cpu().numpy(), scan)
-    else:
-        from bayesopt_smart_amd.acquisition import select_indices
-        idx = select_indices(torch.as_tensor(scan, device="cuda"), cands, ev, q)
+    np.testing.assert_array_equal(acq.cpu().numpy(), scan)
     evs = {tuple(r) for r in ev}
     pts = cands.points(np.arange(n)).astype(np.float64)
     excl = np.array([tuple(p) in evs for p in pts])
