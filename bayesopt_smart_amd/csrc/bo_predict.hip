@@ -485,12 +485,15 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
     if (d->cand_kind == BO_CAND_GRID && !(d->mode & BO_PREDICT_NO_SEPARABLE)) {
       const long long S = d->grid_shape[d->dim - 1];
       const size_t tbl = (size_t)d->n_obj * (2 * S - 1);
-      // per wave: n_obj (cached) or 1 slot of row factors + the int index / on-row arrays
-      const size_t lds_c = base + tbl + (size_t)kWaves * n_pad * (d->n_obj + 1);
+      // per wave: n_obj (cached; + the row's S-bit bitmap of evaluated columns) or 1 slot of row
+      // factors + the int index / on-row arrays
+      const size_t rw_c = (size_t)n_pad * (d->n_obj + 1) + (size_t)(S + 63) / 64;
+      const size_t lds_c = base + tbl + (size_t)kWaves * rw_c;
       const size_t lds_1 = base + tbl + (size_t)kWaves * n_pad * 2;
       if (S % 16 == 0 && S <= 32768 && d->cand_offset % 16 == 0 && lds_1 <= kLdsDoubles) {
         pl->sep = true;
         pl->rw_cache = lds_c <= kLdsDoubles;
+        pl->rw_stride = (int)(pl->rw_cache ? rw_c : (size_t)n_pad * 2);
         pl->off_tbl = (int)base;
         pl->off_rw = (int)(base + tbl);
         lds = pl->rw_cache ? lds_c : lds_1;
@@ -644,6 +647,8 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
       total *= d->grid_shape[k];
     }
     if (d->cand_offset < 0 || d->cand_offset + d->n_cand > total) return BO_ERR_ARG;
+    fa.idx32 = d->cand_offset + d->n_cand < (1LL << 31) ? 1 : 0;
+    for (int k = 0; k < d->dim; ++k) fa.idx32 = fa.idx32 && d->grid_shape[k] < (1LL << 31);
   }
   fa.cand = d->cand;
   if (d->cand_kind == BO_CAND_SOBOL) {
@@ -674,7 +679,8 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     const double ls = d->length_scale[o];
     fa.nhl[o] = -0.5 / (ls * ls);
     fa.beta[o] = d->beta[o];
-    fa.rsq_pv[o] = sqrt(d->prior_var[o]);
+    fa.inv_rsq_pv[o] = 1.0 / sqrt(d->prior_var[o]);
+    fa.inv_pv[o] = 1.0 / d->prior_var[o];
   }
   fa.mu = d->mu;
   fa.var = d->var;
@@ -692,6 +698,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   fa.off_tbl = pl.off_tbl;
   fa.off_rw = pl.off_rw;
   fa.rw_cache = pl.rw_cache ? 1 : 0;
+  fa.rw_stride = pl.rw_stride;
   fa.off_exp = pl.off_exp;
   {
     PrepArgs pa;

@@ -43,7 +43,9 @@ struct FusedArgs {
   unsigned int wpack_bytes;
   int w_pairs;                           // cm: 2-KiB pairs of all objectives' contiguous streams
   const double* alpha;                   // [n_obj][n_pad] = K^-1 (y - pm) (global)
-  double pm[BO_MAX_OBJ], pv[BO_MAX_OBJ], nhl[BO_MAX_OBJ], beta[BO_MAX_OBJ], rsq_pv[BO_MAX_OBJ];
+  double pm[BO_MAX_OBJ], pv[BO_MAX_OBJ], nhl[BO_MAX_OBJ], beta[BO_MAX_OBJ];
+  double inv_rsq_pv[BO_MAX_OBJ], inv_pv[BO_MAX_OBJ];   // 1 / sqrt(pv), 1 / pv (epilogue multiplies)
+  int idx32;                             // grid: every linear index and extent below 2^31
   double *mu, *var, *std_mu, *std_var, *ucb, *acq;
   TopEntry* partial;                     // [gridDim.x * kWaves][topq]
   const double* kstar;                   // KMEM: materialised k_star [n_obj][ks_rows][n_cand]
@@ -56,6 +58,7 @@ struct FusedArgs {
   long long sep_lo;
   int off_tbl, off_rw;
   int rw_cache;                          // SEP row factors kept for every objective (LDS permitting)
+  int rw_stride;                         // doubles of one wave's row-factor region
   int off_exp;                           // LDS offset (doubles) of the 2^(j/256) table
   SobolArgs sob;                         // kind BO_CAND_SOBOL: direction numbers, lo, scale
   const unsigned long long* hkeys;       // hash set of the exclusion rows (excl or xpad), built
@@ -74,6 +77,7 @@ struct Plan {
   bool grows;            // ... training rows / alpha read from global memory (N beyond LDS)
   int off_tbl, off_rw;   // LDS offsets in doubles
   bool rw_cache;         // SEP row factors cached per objective
+  int rw_stride;         // doubles per wave of the row-factor region
   bool fp32;             // cm32_predict_kernel (BO_PREDICT_FP32)
   bool small;            // N <= 128: 4 E-pair accumulators, two workgroups per CU
   int off_exp;
@@ -91,6 +95,14 @@ hipError_t launch_c32_d2(const Plan& pl, const FusedArgs& fa, hipStream_t st);
 hipError_t launch_c32_d4(const Plan& pl, const FusedArgs& fa, hipStream_t st);
 hipError_t launch_c32_d6(const Plan& pl, const FusedArgs& fa, hipStream_t st);
 hipError_t launch_c32_d8(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+// the small-N kernels (MAXEP = 4, two workgroups per CU): bo_predict_s<D>.hip, compiled with the
+// MFMA accumulators in arch VGPRs (-amdgpu-mfma-vgpr-form): in the default split of the 256
+// registers of a 2-waves-per-SIMD kernel (128 VGPR + 128 AGPR) they spilled 40-100 VGPRs to
+// scratch while using 32 of their AGPRs
+hipError_t launch_cms_d2(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_cms_d4(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_cms_d6(const Plan& pl, const FusedArgs& fa, hipStream_t st);
+hipError_t launch_cms_d8(const Plan& pl, const FusedArgs& fa, hipStream_t st);
 
 }  // namespace bo
 
@@ -112,6 +124,19 @@ __device__ __forceinline__ void load_candidate(const FusedArgs& a, long long j, 
   for (int k = 0; k < DIM; ++k) c[k] = 0.0;
   if (!valid) return;
   if (a.cand_kind == BO_CAND_GRID) {
+    if (a.idx32) {                       // 32-bit divisions (the 64-bit ones are ~10x longer)
+      unsigned int gi = (unsigned int)(a.cand_offset + j);
+#pragma unroll
+      for (int k = DIM - 1; k >= 0; --k) {
+        if (k < a.dim) {
+          const unsigned int n = (unsigned int)a.grid_shape[k];
+          const unsigned int q = gi / n;
+          c[k] = (double)(a.grid_lo[k] + (long long)(gi - q * n));
+          gi = q;
+        }
+      }
+      return;
+    }
     long long gi = a.cand_offset + j;
 #pragma unroll
     for (int k = DIM - 1; k >= 0; --k) {
@@ -158,7 +183,12 @@ __device__ __forceinline__ double sqdist(const double* xs, int row, const double
 }
 
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+#ifdef BO_ABL_NOMFMA
+  c.x += a * b;
+  return c;
+#else
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+#endif
 }
 
 // Fence between the last MFMA of a contraction and the first read of its accumulators.
@@ -168,6 +198,12 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 // up to 0.15 pv).  The asm consumes and "redefines" both accumulators in place, so it cannot be
 // scheduled before the MFMAs that produce them and no read of them can be hoisted above it;
 // its 64 wait states cover the MFMA's full latency.
+// (bo_predict_s<D>.hip keeps the accumulators in arch VGPRs: the fence's operand constraint follows)
+#ifdef BO_PREDICT_SMALL_DIM
+#define BO_ACC_AGPR false
+#else
+#define BO_ACC_AGPR true
+#endif
 template <bool AGPR, int NOPS = 64>
 __device__ __forceinline__ void mfma_fence(d4& x, d4& y) {
 #define BO_NOPS8 "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
@@ -349,11 +385,14 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   // SEP row factors, per wave: rv[nslot][n_pad] = pv_o R(f) (one slot per objective when they
   // are cached across the tiles of a grid row, else one slot rebuilt per objective and tile),
   // then rb[n_pad] = table index base (x_f,last - lo_last) + S - 1 and on[n_pad] = "training
-  // point f lies on this grid row" (all other coordinates equal)
+  // point f lies on this grid row" (all other coordinates equal); with the cache, bm = the
+  // row's evaluated columns as a bitmap of S bits (the exclusion is one LDS read per tile)
   const int nslot = a.rw_cache ? a.n_obj : 1;
-  double* rv = smem + a.off_rw + (size_t)wave * a.n_pad * (nslot + 1);
+  double* rv = smem + a.off_rw + (size_t)wave * a.rw_stride;
   int* rb = (int*)(rv + (size_t)nslot * a.n_pad);
   int* on = rb + a.n_pad;
+  unsigned int* bm = (unsigned int*)(on + a.n_pad);
+  const int bm_words = (a.sep_S + 31) >> 5;
   long long cur_row = -1;
   const int TS = 2 * a.sep_S - 1;
   const int nch = a.n_pad / 32;
@@ -381,6 +420,8 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   // distance over the non-last coordinates is shared by the wave's 16 candidates
   auto row_pass = [&](const double (&c)[DIM], int o_lo, int o_hi) {
     __builtin_amdgcn_wave_barrier();
+    if (a.rw_cache)
+      for (int w = lane; w < bm_words; w += 64) bm[w] = 0u;
     for (int f = lane; f < a.n_pad; f += 64) {
       int b = a.sep_S - 1, onrow = 0;                      // padded rows: any in-range index, v = 0
       double sqs = 0.0;
@@ -399,6 +440,8 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         rv[(size_t)(o - o_lo) * a.n_pad + f] = f < a.n_train ? a.pv[o] * exp(sqs * a.nhl[o]) : 0.0;
       rb[f] = b;
       on[f] = onrow;
+      const int col = b - (a.sep_S - 1);
+      if (a.rw_cache && onrow && col >= 0 && col < a.sep_S) atomicOr(bm + (col >> 5), 1u << (col & 31));
     }
     __builtin_amdgcn_wave_barrier();
   };
@@ -416,7 +459,8 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       for (int k = 0; k < DIM; ++k)
         if (k == last) { col0 = (int)(c[k] - (double)a.sep_lo); c[k] += (double)jl; }
       if (a.rw_cache) {
-        const long long row = (a.cand_offset + jj) / a.sep_S;
+        const long long row = a.idx32 ? (long long)((unsigned int)(a.cand_offset + jj) / (unsigned int)a.sep_S)
+                                      : (a.cand_offset + jj) / a.sep_S;
         if (row != cur_row) { row_pass(c, 0, a.n_obj); cur_row = row; }
       }
     } else {
@@ -525,7 +569,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             if constexpr (UPPER) {
 #endif
               if (ch - e0 == e) {
-                mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+                mfma_fence<BO_ACC_AGPR, 64>(acc[e][0], acc[e][1]);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   qpart = __builtin_fma(B[r], acc[e][0][r], qpart);
@@ -572,7 +616,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               const int cur = e & 1, nxt = cur ^ 1;
               const bool more = e + 1 < eN;
               if (more) gq[nxt].s0k(K, e0 + e + 1, g);
-              mfma_fence<true, 64>(acc[e][0], acc[e][1]);
+              mfma_fence<BO_ACC_AGPR, 64>(acc[e][0], acc[e][1]);
               if (more) gq[nxt].s1(K, S[nxt]);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
@@ -595,8 +639,8 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #ifdef BO_ABL_NOEPI
       const double smu = mu - pm, svar = var, u = smu + a.beta[o] * svar;
 #else
-      const double smu = (mu - pm) / a.rsq_pv[o];                      // :563-565
-      const double svar = var / pv;                                    // :568-570
+      const double smu = (mu - pm) * a.inv_rsq_pv[o];                  // :563-565 (x 1/sqrt(pv))
+      const double svar = var * a.inv_pv[o];                           // :568-570 (x 1/pv)
       const double u = smu + a.beta[o] * sqrt(fabs(svar));             // acquisition.py:52
 #endif
       acq = (o == 0) ? u : acq + u;                                    // acquisition.py:108
@@ -624,7 +668,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       const bool need = gi0 >= 0 && bo_better(acq, gi0, tv, ti);
       bool hit = false;
       if (__ballot(need) != 0ull) {
-        if (SEP && !a.excl) {
+        if (SEP && !a.excl && a.rw_cache) {
+          // the row's bitmap of evaluated columns
+          const int col = col0 + jl;
+          hit = valid && ((bm[col >> 5] >> (col & 31)) & 1u);
+        } else if (SEP && !a.excl) {
           // training points on this grid row whose last coordinate falls in the wave's 16
           // columns; OR over the wave, bit jl is this lane's candidate
           unsigned int xmask = 0;
@@ -715,9 +763,12 @@ hipError_t launch_cm_k(const FusedArgs& fa, int grid, size_t lds, hipStream_t st
 template <int DIM, bool UPPER, bool GROWS>
 hipError_t launch_cm_u(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
   if constexpr (GROWS) return launch_cm_k<DIM, false, UPPER, true, bo::kCMaxEp>(fa, pl.grid, pl.lds, st);
-  if (pl.small)
-    return pl.sep ? launch_cm_k<DIM, true, UPPER, false, 4>(fa, pl.grid, pl.lds, st)
-                  : launch_cm_k<DIM, false, UPPER, false, 4>(fa, pl.grid, pl.lds, st);
+  if (pl.small) {
+    if constexpr (DIM == 2) return bo::launch_cms_d2(pl, fa, st);
+    else if constexpr (DIM == 4) return bo::launch_cms_d4(pl, fa, st);
+    else if constexpr (DIM == 6) return bo::launch_cms_d6(pl, fa, st);
+    else return bo::launch_cms_d8(pl, fa, st);
+  }
   return pl.sep ? launch_cm_k<DIM, true, UPPER, false, bo::kCMaxEp>(fa, pl.grid, pl.lds, st)
                 : launch_cm_k<DIM, false, UPPER, false, bo::kCMaxEp>(fa, pl.grid, pl.lds, st);
 }
@@ -886,8 +937,8 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
       const double pv = a.pv[o], pm = a.pm[o];
       const double mu = pm + (double)mpart;                               // :486-488
       const double var = fmax(pv - 2.0 * (double)qpart, BO_MIN_VARIANCE);  // :532-535
-      const double smu = (mu - pm) / a.rsq_pv[o];                         // :563-565
-      const double svar = var / pv;                                       // :568-570
+      const double smu = (mu - pm) * a.inv_rsq_pv[o];                     // :563-565 (x 1/sqrt(pv))
+      const double svar = var * a.inv_pv[o];                              // :568-570 (x 1/pv)
       const double u = smu + a.beta[o] * sqrt(fabs(svar));                // acquisition.py:52
       acq = (o == 0) ? u : acq + u;                                       // acquisition.py:108
       if (valid && g == 0) {
@@ -940,10 +991,23 @@ hipError_t launch_c32(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
 
 }  // namespace
 
-// one translation unit per padded dimension: bo_predict_d<D>.hip defines BO_PREDICT_DIM
-#ifdef BO_PREDICT_DIM
+// one translation unit per padded dimension: bo_predict_d<D>.hip defines BO_PREDICT_DIM;
+// bo_predict_s<D>.hip defines BO_PREDICT_SMALL_DIM (the MAXEP = 4 kernels only)
 #define BO_CAT_(a, b) a##b
 #define BO_CAT(a, b) BO_CAT_(a, b)
+#ifdef BO_PREDICT_SMALL_DIM
+namespace bo {
+hipError_t BO_CAT(launch_cms_d, BO_PREDICT_SMALL_DIM)(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
+  constexpr int D = BO_PREDICT_SMALL_DIM;
+  if (fa.upper)
+    return pl.sep ? launch_cm_k<D, true, true, false, 4>(fa, pl.grid, pl.lds, st)
+                  : launch_cm_k<D, false, true, false, 4>(fa, pl.grid, pl.lds, st);
+  return pl.sep ? launch_cm_k<D, true, false, false, 4>(fa, pl.grid, pl.lds, st)
+                : launch_cm_k<D, false, false, false, 4>(fa, pl.grid, pl.lds, st);
+}
+}  // namespace bo
+#endif
+#ifdef BO_PREDICT_DIM
 namespace bo {
 hipError_t BO_CAT(launch_cm_d, BO_PREDICT_DIM)(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
   return launch_cm<BO_PREDICT_DIM>(pl, fa, st);

@@ -1,0 +1,4 @@
+// Small-N (MAXEP = 4) chunk-major predict kernels for padded input dimension 8, compiled with
+// the MFMA accumulators in arch VGPRs (build.py: -amdgpu-mfma-vgpr-form); see bo_predict_impl.h.
+#define BO_PREDICT_SMALL_DIM 8
+#include "bo_predict_impl.h"

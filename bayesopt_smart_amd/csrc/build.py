@@ -19,12 +19,17 @@ VARIANT = os.environ.get("BO_BUILD_VARIANT", "")      # diagnostic builds: -DBO_
 LIB = os.path.join(PKG, f"libbo_amd{('_' + VARIANT.lower().replace(',', '_')) if VARIANT else ''}.so")
 BUILD = os.path.join(HERE, "build" + (("_" + VARIANT.lower()) if VARIANT else ""))
 SOURCES = ["bo_predict_d2.hip", "bo_predict_d4.hip", "bo_predict_d6.hip", "bo_predict_d8.hip",
+           "bo_predict_s2.hip", "bo_predict_s4.hip", "bo_predict_s6.hip", "bo_predict_s8.hip",
            "bo_predict.hip", "bo_fit.hip", "bo_select.hip", "bo_misc.hip", "bo_hvi.hip"]
 HEADERS = ["bo_common.h", "bo_predict_impl.h", os.path.join("..", "..", "include", "bo_amd.h")]
 ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", os.path.join(ROOT, "include")] + \
         [f"-DBO_ABL_{v}" for v in VARIANT.split(",") if v]
+
+
+# per-source flags: the small-N predict kernels keep their MFMA accumulators in arch VGPRs
+EXTRA = {f"bo_predict_s{d}.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"] for d in (2, 4, 6, 8)}
 
 
 def _hipcc():
@@ -43,7 +48,7 @@ def _compile(src, hdr_mtime):
     o = os.path.join(BUILD, src + ".o")
     if os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), hdr_mtime):
         return o, False
-    cmd = [_hipcc(), *FLAGS, "-c", s, "-o", o]
+    cmd = [_hipcc(), *FLAGS, *EXTRA.get(src, []), "-c", s, "-o", o]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
