@@ -132,13 +132,14 @@ __device__ __forceinline__ void bo_wave_topq_threshold(double lv, long long li, 
 // to their lanes by ds_permute.  Round 1 re-sorted all 64 lanes with a bitonic network (21
 // shuffle stages) whenever a candidate entered -- on spatially coherent acquisition surfaces
 // (a wave walking up a grid row) nearly every tile, ~6 us per tile at C2.
-__device__ __forceinline__ void bo_wave_topq_insert16(double& lv, long long& li, double nv,
-                                                      long long ni, int q) {
+// core: the new entries are (nv, ni) of the lanes 16..47 with `in_new`
+__device__ __forceinline__ void bo_wave_topq_insert_lanes(double& lv, long long& li, double nv,
+                                                          long long ni, bool in_new, int q) {
   const int lane = threadIdx.x & 63;
   double tv;
   long long ti;
   bo_wave_topq_threshold(lv, li, q, tv, ti);
-  const bool beat = (lane >> 4) == 1 && bo_better(nv, ni, tv, ti);
+  const bool beat = in_new && bo_better(nv, ni, tv, ti);
   const unsigned long long nb = __ballot(beat);
   if (nb == 0ull) return;
   const bool isL = lane < q;
@@ -171,6 +172,21 @@ __device__ __forceinline__ void bo_wave_topq_insert16(double& lv, long long& li,
     lv = -__builtin_inf();
     li = -1;
   }
+}
+
+__device__ __forceinline__ void bo_wave_topq_insert16(double& lv, long long& li, double nv,
+                                                      long long ni, int q) {
+  bo_wave_topq_insert_lanes(lv, li, nv, ni, ((threadIdx.x & 63) >> 4) == 1, q);
+}
+
+// Two tiles' 16 candidates at once (lane group 1: (nv1, ni1), lane group 2: (nv2, ni2)): one
+// threshold test, ballot and q broadcast rounds per two tiles.
+__device__ __forceinline__ void bo_wave_topq_insert16x2(double& lv, long long& li, double nv1,
+                                                        long long ni1, double nv2, long long ni2,
+                                                        int q) {
+  const int grp = (threadIdx.x & 63) >> 4;
+  bo_wave_topq_insert_lanes(lv, li, grp == 2 ? nv2 : nv1, grp == 2 ? ni2 : ni1,
+                            grp == 1 || grp == 2, q);
 }
 
 // Hash key of a point for the exclusion of evaluated points (acquisition.py:137-139, exact

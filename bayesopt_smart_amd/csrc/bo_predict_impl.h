@@ -409,6 +409,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 
   double top_v = -__builtin_inf();
   long long top_i = -1;
+  double held_v = -__builtin_inf();     // a tile's candidates waiting for the paired insert
+  long long held_i = -1;
+  bool held = false;
   // SEP: contiguous tile ranges per workgroup, so that a wave walks along grid rows and its
   // row factors are rebuilt once per row (every S / 64 tiles) instead of once per tile;
   // otherwise grid-strided tiles
@@ -696,10 +699,18 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       const bool excluded =
           ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
       const long long gi = excluded ? -1 : gi0;
-      if (a.topq <= 16) bo_wave_topq_insert16(top_v, top_i, acq, gi, a.topq);
-      else bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+      // q <= 16: the tiles are inserted in pairs (the first held in registers; the exclusion
+      // above tested it against the then-current threshold, a lower bound of the later ones)
+      if (a.topq <= 16) {
+        if (held) bo_wave_topq_insert16x2(top_v, top_i, acq, gi, held_v, held_i, a.topq);
+        else { held_v = acq; held_i = gi; }
+        held = !held;
+      } else {
+        bo_wave_topq_insert(top_v, top_i, acq, gi, a.topq);
+      }
     }
   }
+  if (held) bo_wave_topq_insert16(top_v, top_i, held_v, held_i, a.topq);
   BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
   if (a.topq > 0) {
     if (lane < a.topq) {
