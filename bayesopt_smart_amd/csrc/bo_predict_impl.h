@@ -530,6 +530,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             // an XCD's 4 MB L2 (C4: 12.6 MB, C5: 50 MB) otherwise comes from MALL once per
             // wave: C5-f64 1124 -> 869 ms, C4 118.8 -> 116.8 ms (same box).  The SEP path is
             // left unsynchronised (lockstep measured 4 % slower at C3, 7 % at C2: its W fits L2).
+            // (a barrier every 2nd or 4th body measured the same at C4 / C5-f64)
             if constexpr (!SEP) __builtin_amdgcn_s_barrier();
             if constexpr (e == 0) {
               gen.s0(K, al, e0 == 0 && chn != ch, chn, g, An);

@@ -25,7 +25,7 @@ HEADERS = ["bo_common.h", "bo_predict_impl.h", os.path.join("..", "..", "include
 ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", os.path.join(ROOT, "include")] + \
-        [f"-DBO_ABL_{v}" for v in VARIANT.split(",") if v]
+        [(f"-DBO_{v[4:]}" if v.startswith("DEF_") else f"-DBO_ABL_{v}") for v in VARIANT.split(",") if v]
 
 
 # per-source flags: the small-N predict kernels keep their MFMA accumulators in arch VGPRs

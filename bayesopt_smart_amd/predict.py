@@ -253,7 +253,7 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
         raise _lib.BoNativeError(_lib.ERR_ARG, "bo_predict_workspace_size")
     ws = Workspace.get(nbytes, dev)
     res["_keepalive"] = (x_train, y_train, kinv, excl_points)
-    call = PreparedPredict(lib, desc, ws, stream_handle(dev), res)
+    call = PreparedPredict(lib, desc, ws, stream_handle(dev), res, dev)
     return call if prepare else call()
 
 
@@ -264,14 +264,39 @@ class PreparedPredict:
     between calls.  Like a library plan object, it skips only the host-side validation and the
     descriptor build of predict_acquire (tens of microseconds of Python per call)."""
 
-    def __init__(self, lib, desc, ws, stream, res):
+    def __init__(self, lib, desc, ws, stream, res, dev=None):
         self._lib, self._desc, self._ws, self._stream, self.res = lib, desc, ws, stream, res
         self._ws_ptr, self._ws_n = ws.data_ptr(), ws.numel()
+        self._dev = dev
 
     def __call__(self):
         _lib.check(self._lib.bo_predict_acquire(self._desc, self._ws_ptr, self._ws_n, self._stream),
                    "bo_predict_acquire")
         return self.res
+
+    def graphed(self):
+        """The same call captured once as a HIP graph (preparation, fused kernel, merge): each
+        replay is one graph launch from the host instead of three kernel launches, and the
+        kernels start back to back.  Replays run on the current stream; the library's kernel
+        timer (bo_profile_start/stop) does not see them."""
+        dev = self._dev
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            _lib.check(self._lib.bo_predict_acquire(self._desc, self._ws_ptr, self._ws_n, side.cuda_stream),
+                       "bo_predict_acquire")
+            with torch.cuda.graph(g, stream=side, capture_error_mode="relaxed"):
+                _lib.check(self._lib.bo_predict_acquire(self._desc, self._ws_ptr, self._ws_n,
+                                                        side.cuda_stream), "bo_predict_acquire")
+        torch.cuda.current_stream(dev).wait_stream(side)
+        res = self.res
+
+        def replay():
+            g.replay()
+            return res
+        replay.graph = g
+        return replay
 
 
 def merge_topq(vals, idxs, q):
