@@ -235,14 +235,15 @@ def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, budget_s=20.0,
     return res, acq, cpu_sel
 
 
-def pmc_traffic():
-    """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary, if any."""
+def pmc_traffic(workload="C3"):
+    """HBM bytes per fused-kernel launch from the newest committed rocprofv3 PMC summary of this
+    workload (profiles/*pmc*.json, scripts/pmc_summary.py), if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     for f in reversed(files):
         try:
             with open(f) as fh:
                 d = json.load(fh)
-            if d.get("workload") == "C3" and d.get("hbm_bytes_per_launch"):
+            if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
                 return float(d["hbm_bytes_per_launch"])
         except Exception:
             pass
@@ -497,7 +498,7 @@ def main():
         # algorithmic HBM bytes per candidate: outputs written (+ explicit coordinates read)
         n_out = sum(1 if k == "acq" else n_obj for k in outputs)
         alg_bytes = (8 * n_out + (0 if cand[0] == "grid" else 8 * d)) * per_rank
-        traffic = pmc_traffic() if args.config == "C3" and args.mode == "auto" and args.acq == "sum_ucb" else None
+        traffic = pmc_traffic(args.config) if args.mode == "auto" and args.acq == "sum_ucb" else None
         res = {
             "metric": metric,
             "value": total / t_step,
