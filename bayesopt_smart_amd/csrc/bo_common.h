@@ -289,18 +289,23 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
   __shared__ int s_cnt, s_nl;
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) { s_cnt = 0; s_nl = 0; }
+  // the heads of lists tid + u nt, u < 16, stay in registers for the second pass (all of them
+  // up to 16 x 256 = 4096 lists); more lists are re-read
+  constexpr int HC = 16;
+  TopEntry hd[HC];
   double bv = -__builtin_inf();
   long long bi = -1;
-  for (long long l0 = tid; l0 < n_lists; l0 += 4 * nt) {
-    TopEntry e[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long long l = l0 + (long long)u * nt;
-      e[u] = l < n_lists ? L[l * q] : TopEntry{-__builtin_inf(), -1};
-    }
+  for (int u = 0; u < HC; ++u) {
+    const long long l = tid + (long long)u * nt;
+    hd[u] = l < n_lists ? L[l * q] : TopEntry{-__builtin_inf(), -1};
+  }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (bo_better(e[u].v, e[u].i, bv, bi)) { bv = e[u].v; bi = e[u].i; }
+  for (int u = 0; u < HC; ++u)
+    if (bo_better(hd[u].v, hd[u].i, bv, bi)) { bv = hd[u].v; bi = hd[u].i; }
+  for (long long l = tid + (long long)HC * nt; l < n_lists; l += nt) {
+    const TopEntry e = L[l * q];
+    if (bo_better(e.v, e.i, bv, bi)) { bv = e.v; bi = e.i; }
   }
   bo_wave_sort64(bv, bi);
   {
@@ -312,7 +317,15 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
   TopEntry T = s_red[0];
   for (int w = 1; w < (nt >> 6); ++w)
     if (bo_better(s_red[w].v, s_red[w].i, T.v, T.i)) T = s_red[w];
-  for (long long l = tid; l < n_lists; l += nt) {
+#pragma unroll
+  for (int u = 0; u < HC; ++u) {
+    const long long l = tid + (long long)u * nt;
+    if (l < n_lists && hd[u].i >= 0 && !bo_better(T.v, T.i, hd[u].v, hd[u].i)) {
+      const int p = atomicAdd(&s_nl, 1);
+      if (p < BO_MERGE_CAP) s_lists[p] = (int)l;
+    }
+  }
+  for (long long l = tid + (long long)HC * nt; l < n_lists; l += nt) {
     const TopEntry e = L[l * q];
     if (e.i >= 0 && !bo_better(T.v, T.i, e.v, e.i)) {
       const int p = atomicAdd(&s_nl, 1);

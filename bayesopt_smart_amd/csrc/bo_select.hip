@@ -243,6 +243,17 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
   const unsigned long long* hk = a.hkeys;
   const int* hi = a.hidx;
   unsigned int hm = a.hmask;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long b_first = (long long)blockIdx.x * blockDim.x + wave * 64;
+  // M == 0: the first step's loads are issued before the hash build (they need no table)
+  double pre[U];
+  if constexpr (M == 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long j = b_first + u * stride + lane;
+      pre[u] = j < a.n_cand ? a.acq[j] : 0.0;
+    }
+  }
   if (a.lds_slots > 0) {
     int* lidx = (int*)(lkeys + a.lds_slots);
     for (int t = tid; t < a.lds_slots; t += blockDim.x) lkeys[t] = 0ull;
@@ -259,9 +270,8 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
   double lv = -__builtin_inf(), tv = -__builtin_inf();   // list entry; the list's q-th (uniform)
   long long li = -1, ti = -1;
   const unsigned long long below = (1ull << lane) - 1ull;
-  const long long stride = (long long)gridDim.x * blockDim.x;
   // wave-uniform trip count: every lane stays in the loop for the ballots and broadcasts
-  for (long long b0 = (long long)blockIdx.x * blockDim.x + wave * 64; b0 < a.n_cand; b0 += U * stride) {
+  for (long long b0 = b_first; b0 < a.n_cand; b0 += U * stride) {
     double val[U];
     bool any = false;
 #pragma unroll
@@ -269,7 +279,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
       const long long j = b0 + u * stride + lane;
       const bool in = j < a.n_cand;
       if constexpr (M == 0) {
-        val[u] = in ? a.acq[j] : 0.0;
+        val[u] = b0 == b_first ? pre[u] : (in ? a.acq[j] : 0.0);
       } else {
         double p[M];
         bool nan = false;
