@@ -542,7 +542,7 @@ def main():
             res["front_hypervolume"] = {"value": hv_front, "reference_point": ref_pt.tolist(),
                                         "method": f"bo_box_volume_sum over this rank's share of the "
                                                   f"{n_boxes[0]} boxes + all_reduce(SUM) over {world} rank(s)"}
-            res["hvi_select"] = {"kernels": f"select_lane_kernel<{8 if q <= 4 else 16 if q <= 12 else 24}, {n_obj}> "
+            res["hvi_select"] = {"kernels": f"select_stream_kernel<{n_obj}, 4> "
                                             "+ bo_topq_merge_kernel (exact HVI + top-q, one pass)",
                                  "ms": hms, "n_boxes": n_boxes[0], "front_points": int(front_y.shape[0]),
                                  "bytes_per_candidate": 8 * n_obj + 8,
