@@ -224,10 +224,11 @@ __device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff
   return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+template <int PF>
 __device__ __forceinline__ void prime_ring(__amdgpu_buffer_rsrc_t wr, int voff, int base,
-                                           d2 (&wa)[kPF], d2 (&wb)[kPF]) {
+                                           d2 (&wa)[PF], d2 (&wb)[PF]) {
 #pragma unroll
-  for (int p = 0; p < kPF; ++p) {
+  for (int p = 0; p < PF; ++p) {
     wa[p] = wload(wr, voff, base + (p << 11));
     wb[p] = wload(wr, voff, base + (p << 11) + 1024);
   }
@@ -372,9 +373,16 @@ struct KGen {
 // GROWS: the training rows, |x_f|^2 and alpha are read from global memory (L2-resident)
 // instead of LDS, for N whose rows do not fit the 160 KiB LDS (the reference has no N cap).
 // ---------------------------------------------------------------------------------------
+#ifndef BO_SMALL_PF
+#define BO_SMALL_PF 2
+#endif
 template <int DIM, bool SEP, bool UPPER, bool GROWS, int MAXEP>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   constexpr bool upper = UPPER;
+  // W ring depth in pairs of k-steps: kPF, or BO_SMALL_PF = 2 for the small-N kernels (their W
+  // is L2-resident; 16 VGPRs fewer: C2 spills 39 -> 4 VGPRs, kernel -1.3 %)
+  constexpr int PF = MAXEP <= 4 ? BO_SMALL_PF : kPF;
+  static_assert(4 % PF == 0, "the ring depth divides the 4 pairs of an E-pair body");
   // training rows (SEP: original grid coordinates; otherwise centred on z = row 0), alpha
   const double* xs = GROWS ? a.xc : smem;
   const double* alpha = GROWS ? a.alpha : smem + (size_t)a.n_pad * DIM;
@@ -488,7 +496,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       // at the end of the packed streams, measured 1.7 % slower at C4 and 3 % faster at C2 on
       // one box: its modular refill offsets defeat the immediate-offset addressing)
       const int base = o * w_obj;
-      d2 wa[kPF], wb[kPF];
+      d2 wa[PF], wb[PF];
       prime_ring(wr, voff, base, wa, wb);
       int pos = 0;
       double mpart = 0.0, qpart = 0.0;
@@ -539,13 +547,14 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #pragma unroll
             for (int pp = 0; pp < 4; ++pp) {
               // MFMAs first, then the refill of the same ring slot (no operand copies)
-              acc[e][0] = mfma64(wa[pp].x, B[2 * pp], acc[e][0]);
-              acc[e][1] = mfma64(wb[pp].x, B[2 * pp], acc[e][1]);
-              acc[e][0] = mfma64(wa[pp].y, B[2 * pp + 1], acc[e][0]);
-              acc[e][1] = mfma64(wb[pp].y, B[2 * pp + 1], acc[e][1]);
-              const int so = base + ((pos + kPF) << 11);
-              wa[pp] = wload(wr, voff, so);
-              wb[pp] = wload(wr, voff, so + 1024);
+              const int sl = pp % PF;         // ring slot (PF divides the 4 pairs of a body)
+              acc[e][0] = mfma64(wa[sl].x, B[2 * pp], acc[e][0]);
+              acc[e][1] = mfma64(wb[sl].x, B[2 * pp], acc[e][1]);
+              acc[e][0] = mfma64(wa[sl].y, B[2 * pp + 1], acc[e][0]);
+              acc[e][1] = mfma64(wb[sl].y, B[2 * pp + 1], acc[e][1]);
+              const int so = base + ((pos + PF) << 11);
+              wa[sl] = wload(wr, voff, so);
+              wb[sl] = wload(wr, voff, so + 1024);
               ++pos;
               if constexpr (e == 0) {
                 if (pp == 0) {
