@@ -426,7 +426,12 @@ def main():
 
     # the prepared call replayed as a HIP graph (one launch per step from the host); the
     # library's kernel timer runs over separate non-graph calls after the timed region
-    run = predict.graphed() if (args.acq != "hvi" and not args.no_graph) else predict
+    run, step_launch = predict, "direct"
+    if args.acq != "hvi" and not args.no_graph:
+        try:
+            run, step_launch = predict.graphed(), "hip_graph"
+        except Exception as exc:  # capture unsupported here: launch directly (stated in the line)
+            print(f"[bench] HIP graph capture failed ({exc}); launching directly", file=sys.stderr)
 
     def step():
         if args.acq == "hvi":
@@ -515,7 +520,7 @@ def main():
                      "synthetic (toy_function_3d on a seeded design drawn from the Sobol set)"),
             "config": {"workload": cfg["workload"], "n_train": n, "n_cand_per_gpu": per_rank,
                        "n_cand_total": total, "n_objectives": n_obj, "dim": d, "topq": q,
-                       "parallelism": f"candidate-shard x{world}"},
+                       "parallelism": f"candidate-shard x{world}", "step_launch": step_launch},
             "roofline": {"bound": "mfma", "achieved": executed, "peak": peak, "unit": "TFLOP/s",
                          "frac": executed / peak,
                          "flops_basis": f"executed MFMA flops per candidate ({fx}; "
