@@ -25,11 +25,16 @@ HEADERS = ["bo_common.h", "bo_predict_impl.h", os.path.join("..", "..", "include
 ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I", os.path.join(ROOT, "include")] + \
-        [(f"-DBO_{v[4:]}" if v.startswith("DEF_") else f"-DBO_ABL_{v}") for v in VARIANT.split(",") if v]
+        [(f"-DBO_{v[4:]}" if v.startswith("DEF_") else f"-DBO_ABL_{v}") for v in VARIANT.split(",") if v] + \
+        os.environ.get("BO_EXTRA_FLAGS", "").split()   # diagnostic builds (with a VARIANT name)
 
 
-# per-source flags: the small-N predict kernels keep their MFMA accumulators in arch VGPRs
+# per-source flags: the small-N predict kernels keep their MFMA accumulators in arch VGPRs; the
+# 2-D translation units (the integer-grid configs C2/C3) use the max-ILP machine scheduler
+# (same-box A/B: C2 -1.5 %, C3 -0.5 %; on the 6-D Sobol kernel of C4 it measured +4.5 %)
 EXTRA = {f"bo_predict_s{d}.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"] for d in (2, 4, 6, 8)}
+for _src in ("bo_predict_d2.hip", "bo_predict_s2.hip"):
+    EXTRA[_src] = EXTRA.get(_src, []) + ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 
 
 def _hipcc():
