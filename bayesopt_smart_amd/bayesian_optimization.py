@@ -83,7 +83,7 @@ def _predict_select(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, lengt
     q = batch_size if batch_size <= _lib.MAX_TOPQ and acquisition == "sum_ucb" else 0
     r = predict_acquire(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
                         outputs=tuple(out), topq=q, out=out)
-    if acquisition == "hvi" and batch_size <= 16:
+    if acquisition == "hvi" and batch_size <= _lib.MAX_TOPQ:
         # exact HVI and its top-q with exclusion in one device pass
         idx = hvi_select_indices(buffers.acquisition_values, buffers.ucb, y_evaluated, len(y_evaluated),
                                  reference_point, prior_mean, prior_variance, cands, evaluated, batch_size)
@@ -189,11 +189,14 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
     return x_vector, y_vector, last_eval + 1
 
 
-def _check_limits(n_obj, dim, total_samples, batch_size):
+def _check_limits(n_obj, dim, total_samples, batch_size, acquisition="sum_ucb"):
     """Fail in the constructor -- before any objective evaluation -- on shapes the device path
     cannot run (the reference would hit them only mid-loop, if at all)."""
     if not 1 <= n_obj <= _lib.MAX_OBJ:
         raise ValueError(f"n_objectives must be in [1, {_lib.MAX_OBJ}] (got {n_obj})")
+    if acquisition == "hvi" and n_obj > 4:
+        raise ValueError(f"acquisition='hvi' supports at most 4 objectives (got {n_obj}): the exact "
+                         "hypervolume improvement's box decomposition is limited to n_obj <= 4")
     if not 1 <= dim <= _lib.MAX_DIM:
         raise ValueError(f"the input dimension must be in [1, {_lib.MAX_DIM}] (got {dim})")
     if batch_size < 1:
@@ -242,7 +245,10 @@ class BayesianOptimization:
                            else CandidateSet.explicit(explicit, self.device))
         self._input_space = None
         self.total_samples = self.initial_samples + self.n_iterations * self.batch_size
-        _check_limits(n_objectives, self.dim, self.total_samples, self.batch_size)
+        self.acquisition = kwargs.get("acquisition", "sum_ucb")
+        if self.acquisition not in ("sum_ucb", "hvi"):
+            raise ValueError(f"unknown acquisition {self.acquisition!r} (expected 'sum_ucb' or 'hvi')")
+        _check_limits(n_objectives, self.dim, self.total_samples, self.batch_size, self.acquisition)
         self.x_vector = np.zeros((self.total_samples, self.dim), dtype=NUMBA_FLOAT_TYPE)
         self.y_vector = np.zeros((self.total_samples, n_objectives), dtype=NUMBA_FLOAT_TYPE)
         self._buffers = DeviceBuffers(n_objectives, self.total_samples, self.candidates.n, self.device)
@@ -256,9 +262,6 @@ class BayesianOptimization:
             self.prior_variance = K.compute_prior_variance(self.y_vector, self.n_evaluations, n_objectives)
         self.reference_point = np.array(kwargs.get("reference_point", [0.0] * n_objectives),
                                         dtype=NUMBA_FLOAT_TYPE)
-        self.acquisition = kwargs.get("acquisition", "sum_ucb")
-        if self.acquisition not in ("sum_ucb", "hvi"):
-            raise ValueError(f"unknown acquisition {self.acquisition!r} (expected 'sum_ucb' or 'hvi')")
 
     # the reference's preallocated arrays, materialised on the host on demand
     @property

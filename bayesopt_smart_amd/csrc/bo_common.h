@@ -16,6 +16,23 @@ typedef double d4 __attribute__((ext_vector_type(4)));
     if (_e != hipSuccess) return BO_ERR_HIP;       \
   } while (0)
 
+// Bounds checks of the diagnostic build (BO_BUILD_VARIANT=DEF_DEBUG_BOUNDS -> -DBO_DEBUG_BOUNDS):
+// every checked index is printed when out of range and the access is skipped, so that a bad
+// index names itself instead of faulting the device.  The release build compiles them away.
+#ifdef BO_DEBUG_BOUNDS
+#include <stdio.h>
+__device__ __forceinline__ bool bo_bound(bool ok, const char* what, long long v, long long cap, int line) {
+  if (!ok)
+    printf("BO_DEBUG_BOUNDS line %d: %s = %lld outside [0, %lld) (block %d, thread %d)\n", line, what, v, cap,
+           (int)blockIdx.x, (int)threadIdx.x);
+  return ok;
+}
+#define BO_IN(v, cap, what) bo_bound((long long)(v) >= 0 && (long long)(v) < (long long)(cap), what, \
+                                     (long long)(v), (long long)(cap), __LINE__)
+#else
+#define BO_IN(v, cap, what) true
+#endif
+
 // MIN_VARIANCE / KERNEL_JITTER / CHOLESKY_JITTER: bayesopt/config.py:57-66 (fp64 branch).
 #define BO_MIN_VARIANCE 1e-10
 #define BO_KERNEL_JITTER 1e-6
@@ -220,13 +237,13 @@ __device__ __forceinline__ void bo_hash_insert(unsigned long long* keys, int* id
 // Is point c (dim coordinates) one of the rows of pts ([*][ld]) stored in the table?
 __device__ __forceinline__ bool bo_hash_contains(const unsigned long long* keys, const int* idx,
                                                  unsigned int mask, const double* pts, int ld,
-                                                 const double* c, int dim) {
+                                                 const double* c, int dim, long long n_pts = 1ll << 40) {
   const unsigned long long key = bo_point_key(c, dim);
   if (key == 0ull) return false;
   for (unsigned int t = (unsigned int)key & mask;; t = (t + 1) & mask) {
     const unsigned long long kt = keys[t];
     if (kt == 0ull) return false;
-    if (kt == key) {
+    if (kt == key && BO_IN(idx[t], n_pts, "hash idx[t]")) {
       const double* r = pts + (long long)idx[t] * ld;
       bool eq = true;
 #pragma unroll
@@ -343,7 +360,8 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
     int P = 1;
     while (P < nl) P <<= 1;
     for (int k = tid; k < P; k += nt)
-      s_buf[k] = k < nl ? L[(long long)s_lists[k] * q] : TopEntry{-__builtin_inf(), -1};
+      if (BO_IN(k, BO_MERGE_CAP, "merge s_buf[k] (heads)"))
+        s_buf[k] = k < nl ? L[(long long)s_lists[k] * q] : TopEntry{-__builtin_inf(), -1};
     __syncthreads();
     for (int k2 = 2; k2 <= P; k2 <<= 1)
       for (int j = k2 >> 1; j > 0; j >>= 1) {
@@ -367,7 +385,10 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
     for (int k = tid; k < nl; k += nt) {
       const int l = s_lists[k];
       const TopEntry h = L[(long long)l * q];
-      if (h.i >= 0 && !bo_better(T.v, T.i, h.v, h.i)) s_lists2[atomicAdd(&s_nl2, 1)] = l;
+      if (h.i >= 0 && !bo_better(T.v, T.i, h.v, h.i)) {
+        const int p2 = atomicAdd(&s_nl2, 1);
+        if (BO_IN(p2, BO_MERGE_CAP, "merge s_lists2")) s_lists2[p2] = l;
+      }
     }
     __syncthreads();
     nl = s_nl2;
@@ -375,6 +396,7 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
   }
   if (nl <= BO_MERGE_CAP) {
     for (int k = tid; k < nl * q; k += nt) {
+      if (!BO_IN(lists[k / q], n_lists, "merge lists[k / q]")) continue;
       const TopEntry e = L[(long long)lists[k / q] * q + k % q];
       if (e.i >= 0 && !bo_better(T.v, T.i, e.v, e.i)) {
         const int p = atomicAdd(&s_cnt, 1);
@@ -388,7 +410,7 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
         const TopEntry me = s_buf[k];
         int rank = 0;
         for (int m = 0; m < cnt; ++m) rank += bo_better(s_buf[m].v, s_buf[m].i, me.v, me.i) ? 1 : 0;
-        if (rank < q) { out_v[rank] = me.v; out_i[rank] = me.i; }
+        if (rank < q && BO_IN(rank, q, "merge rank")) { out_v[rank] = me.v; out_i[rank] = me.i; }
       }
       for (int t = cnt + tid; t < q; t += nt) { out_v[t] = -__builtin_inf(); out_i[t] = -1; }
       return;

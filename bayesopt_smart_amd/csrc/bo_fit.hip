@@ -1,34 +1,42 @@
-// GP fit on device: compute_mll and invert_k on one blocked, MFMA-backed Cholesky.
+// GP fit on device: compute_mll and invert_k on one blocked right-looking Cholesky, one kernel
+// launch per 32-column step.
 //
 //   bo_compute_mll  numba_kernels.py:152-235   sum over objectives of the GP marginal log
 //                   likelihood of K/pv + 1e-8 I with y centred on the prior mean and scaled by
 //                   its population std.
 //   bo_invert_k     numba_kernels.py:370-403   inv(K + 1e-6 I) per objective (the reference's
-//                   LAPACK gesv); Cholesky first, Gauss-Jordan with partial pivoting (LAPACK's
-//                   idamax row choice) for any objective whose Cholesky fails.
+//                   LAPACK gesv); Cholesky first, blocked LU with partial pivoting (LAPACK's
+//                   getrf row choice) for any objective whose Cholesky fails or whose K is not
+//                   symmetric.
 //
-// One factorisation serves both: the right-looking blocked Cholesky (64 x 64 tiles) of an
-// AUGMENTED lower-triangular matrix
+// One factorisation serves both: the Cholesky of an AUGMENTED lower-triangular matrix
 //
 //        [ K    .  ]      factoring only the first n_p columns leaves     [ L          .          ]
-//    A = [ B    C  ]      (n_p = N padded to 64 with an identity block)   [ B L^-T     C - B K^-1 B^T ]
+//    A = [ B    C  ]      (n_p = N padded to 32 with an identity block)   [ B L^-T     C - B K^-1 B^T ]
 //
-//   * compute_mll: B = yc^T (one row), C = 0:  the bottom row holds z = L^-1 yc and the corner
-//     holds -yc^T K^-1 yc, the data-fit term (numba_kernels.py:216-222: solve(L, yc),
-//     solve(L^T, .), yc . alpha); log det = 2 sum log L_ii (:225-229);
-//   * invert_k:    B = I, C = 0:  the bottom-right block holds -K^-1 (lower triangle); the zero
-//     blocks of L^-T (upper triangular) are skipped, so the whole inverse costs about 3/2 of a
-//     Cholesky of the 2N system's first half.
+//   * compute_mll: B = (y - pm)^T (one row), no C:  the bottom row becomes z = L^-1 (y - pm), so
+//     |z|^2 / var(y) is the data-fit term yc . alpha of :216-222 (yc = (y - pm) / std), and
+//     log det = 2 sum log L_ii (:225-229);
+//   * invert_k:    B = I, C = 0:  the bottom-right block becomes -K^-1 (lower triangle).  B L^-T
+//     is upper triangular: bottom row block b is structurally zero in column blocks < b, and C's
+//     tile (b, c) receives its first contribution at step b (no zero fill).
 //
-// A is stored COLUMN-major (element (i, j) of the lower triangle at j * Na + i), so that the
-// row-per-lane accesses of the panel kernel and the row-contiguous tile loads of the update are
-// coalesced.  Per 64-column step k: chol_panel_kernel factors the diagonal tile (one wave, one
-// row per lane) and solves the tiles below it (row substitution, one row per lane; 4 row blocks
-// per workgroup); chol_update_kernel applies A_pq -= L_pk L_qk^T to every live tile of the
-// trailing matrix with v_mfma_f64_16x16x4_f64 (64 x 64 x 64 per workgroup).  A non-positive or NaN pivot
-// sets the objective's status (compute_mll: BO_ERR_NOT_PD = LinAlgError, as cholesky raises at
-// :214; invert_k: the LU fallback).  Sizes are not capped: the workspace is n_obj (N + 64)^2
-// doubles (MLL) or n_obj (2 N_p)^2 (inverse).
+// A is COLUMN-major (element (i, j) at j * Na + i) and lives in the workspace.  Launch k (32-column
+// step k, one launch per step; the kernel boundary is the only synchronisation) runs two roles:
+//   * panel (column block k): every panel workgroup applies step k-1's update to the diagonal
+//     tile and to ITS 32-row slab (MFMA, 4 waves), then wave 0 factors the diagonal tile and
+//     solves its slab rows in the same register sweep -- lanes 0..31 hold the diagonal rows,
+//     lanes 32..63 the slab rows, one row per lane: column j's pivot is a v_readlane, its
+//     entries below the diagonal are both L_jj^-1 a_j for the tile and the triangular solve of
+//     the slab (X L_kk^T = A_pk), and the next column is updated first so that the chain per
+//     column is readlane -> rsqrt -> mul -> readlane -> fma.  Every panel workgroup factors the
+//     diagonal tile redundantly (no inter-workgroup hand-off inside the launch);
+//   * update (column blocks > k, and C for the inverse): A_pc -= L_p,k-1 L_c,k-1^T for every live
+//     32 x 32 tile, one tile per wave (32 v_mfma_f64_16x16x4_f64), applying step k-1 one launch
+//     late (lookahead: the panel of step k needs only its own column block).
+// The critical path per step is one panel: ~0.4 us of MFMA, a 32-column register factorisation
+// and the kernel boundary.  Round 2 used two launches per 64-column step with a 64-long serial
+// substitution chain on one wave (45 us per panel at N = 2048).
 
 #include "bo_common.h"
 
@@ -39,294 +47,420 @@
 
 namespace {
 
-constexpr int NB = 64;      // tile size
-constexpr int LS = 66;      // LDS row stride (doubles) of staged tiles
+constexpr int NB = 32;      // column block (panel width) and update tile
+constexpr int CS = 33;      // LDS row stride (doubles) of the panel tile
 
 struct FitParams {
-  double pv[BO_MAX_OBJ], pm[BO_MAX_OBJ], ls2[BO_MAX_OBJ], jitter, scale_by_pv;
+  double pv[BO_MAX_OBJ], pm[BO_MAX_OBJ], ls2[BO_MAX_OBJ], jitter;
 };
 
-// Geometry of the augmented system: top part n_p = nbt * 64 rows (N padded), bottom part
-// rb * 64 rows; leading dimension Na = n_p + 64 rb.  ident: B = I (structurally upper-triangular
-// bottom-left tiles, inverse); otherwise every bottom tile is live (MLL).
-struct Aug {
-  int n, nbt, rb, ident;
-  long long Na;
+// Geometry of the augmented system (per objective): K part n_p = 32 nbt rows/columns; bottom
+// rows 32 (MLL: row n_p = y - pm) or n_p (inverse: B = I); columns n_p (MLL) or 2 n_p (inverse:
+// the C block).  ostride = Na * ncols doubles per objective.
+struct Geo {
+  int n, nbt, ident, n_obj;
+  long long Na, ncols, ostride;
 };
 
-// --------------------------------------------------------------------------- init
-// Lower triangle of the augmented matrix, per objective (blockIdx.y), column j = blockIdx.x,
-// rows i >= j over the threads (coalesced column-major writes):
-//   i, j < N:           MLL: v / pv + 1e-8 d_ij with v = pv exp(-0.5 |x_i - x_j|^2 / ls^2) exactly
-//                       as update_k (numba_kernels.py:352-361), also written to the caller's
-//                       kernel_matrix (both triangles, the reference rebuilds it in compute_mll);
-//                       inverse: K[i][j] + 1e-6 d_ij from the caller's kernel_matrix;
-//   padding of K:       identity;
-//   bottom rows:        MLL: row n_p = yc (ycv), the rest 0; inverse: B = I; C = 0.
-__global__ __launch_bounds__(256) void aug_init_kernel(double* __restrict__ A, Aug g,
-                                                      double* __restrict__ km, long long ld,
-                                                      const double* __restrict__ x, int dim,
-                                                      const double* __restrict__ ycv, FitParams p,
-                                                      int gram) {
-  const int o = blockIdx.y;
-  const long long j = blockIdx.x;
+// per-objective partials of the MLL: [2 nbt + 1] doubles (log det partial per step, |z|^2
+// partial per step, var(y - pm)); statuses after all objectives' partials
+__host__ __device__ inline int part_len(const Geo& g) { return 2 * g.nbt + 1; }
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// 1 / sqrt(x): v_rsq_f64 and two Newton steps (NaN for x <= 0 or NaN: the caller flags the pivot)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double r = __builtin_fma(-x * y, y, 1.0);
+  y = __builtin_fma(0.5 * y, r, y);
+  r = __builtin_fma(-x * y, y, 1.0);
+  return __builtin_fma(0.5 * y, r, y);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// triangular index t -> row u, t = u (u + 1) / 2 + rest
+__device__ __forceinline__ int tri_row(long long t) {
+  int u = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((long long)(u + 1) * (u + 2) / 2 <= t) ++u;
+  while ((long long)u * (u + 1) / 2 > t) --u;
+  return u;
+}
+
+// ------------------------------------------------------------------------------- init
+// Lower 32 x 32 tiles of the augmented matrix (one workgroup per tile, linear tile index over the
+// lower triangle of the K part, then the bottom tiles that are live in their column block).
+//   K part (i, j < N):  MLL: v / pv + 1e-8 d_ij with v = pv exp(-0.5 |x_i - x_j|^2 / ls^2) exactly
+//                       as update_k (numba_kernels.py:352-361), v also stored to the caller's
+//                       kernel_matrix in both triangles (compute_mll rebuilds it, :178-185);
+//                       inverse: K[i][j] + 1e-6 d_ij from the caller's kernel_matrix, with
+//                       K[i][j] == K[j][i] checked (an asymmetric K takes the LU path);
+//   K padding:          identity;
+//   bottom:             MLL: row n_p = y_j - pm (j < N), the rest 0; inverse: B = I on the live
+//                       tiles (bottom block b in column block j >= b).
+// Extra workgroups (MLL, one per objective) compute var(y - pm), population (np.std squared).
+__global__ __launch_bounds__(256) void fit_init_kernel(double* __restrict__ A, Geo g,
+                                                       double* __restrict__ km, long long ld,
+                                                       const double* __restrict__ x, int dim,
+                                                       const double* __restrict__ y, long long ld_y,
+                                                       FitParams p, double* __restrict__ part,
+                                                       int* __restrict__ status, int tiles_per_obj) {
+  __shared__ double tile[NB][NB + 1];
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
   const long long np_ = (long long)g.nbt * NB;
-  double* Ao = A + (long long)o * g.Na * g.Na;
-  double* ko = km + (long long)o * ld * ld;
-  for (long long i = j + threadIdx.x; i < g.Na; i += blockDim.x) {
-    double v = 0.0;
-    if (i < np_) {
-      if (i < g.n && j < g.n) {
-        double kv;
-        if (gram) {
+  if ((int)blockIdx.x >= g.n_obj * tiles_per_obj) {
+    // var(y - pm) of one objective (two passes, as np.std)
+    const int o = blockIdx.x - g.n_obj * tiles_per_obj;
+    double s = 0.0;
+    for (int i = tid; i < g.n; i += 256) s += y[(long long)i * ld_y + o] - p.pm[o];
+    red[tid] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) { if (tid < w) red[tid] += red[tid + w]; __syncthreads(); }
+    const double mean = red[0] / g.n;
+    __syncthreads();
+    s = 0.0;
+    for (int i = tid; i < g.n; i += 256) {
+      const double d = (y[(long long)i * ld_y + o] - p.pm[o]) - mean;
+      s += d * d;
+    }
+    red[tid] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) { if (tid < w) red[tid] += red[tid + w]; __syncthreads(); }
+    if (tid == 0) part[(long long)o * part_len(g) + 2 * g.nbt] = red[0] / g.n;
+    return;
+  }
+  const int o = blockIdx.x / tiles_per_obj;
+  long long t = blockIdx.x % tiles_per_obj;
+  const long long tri = (long long)g.nbt * (g.nbt + 1) / 2;
+  int ti, tj;                                  // tile row / column block
+  if (t < tri) {
+    ti = tri_row(t);
+    tj = (int)(t - (long long)ti * (ti + 1) / 2);
+  } else {                                      // bottom tiles
+    t -= tri;
+    if (g.ident) {                              // (nbt + b, j) for b <= j: column-wise triangle
+      const int u = tri_row(t);
+      tj = u;
+      ti = g.nbt + (int)(t - (long long)u * (u + 1) / 2);
+    } else {
+      ti = g.nbt;
+      tj = (int)t;
+    }
+  }
+  double* Ao = A + (long long)o * g.ostride;
+  const long long r0 = (long long)ti * NB, c0 = (long long)tj * NB;
+  const int c = tid >> 5, r = tid & 31;         // column-major writes: lane r = row, c + 8 pass
+  if (ti < g.nbt) {
+    // K part: values into the LDS tile [row][col]
+    if (!g.ident) {
+      double* ko = km + (long long)o * ld * ld;
+      for (int e = tid; e < NB * NB; e += 256) {
+        const int rr = e >> 5, cc = e & 31;     // row rr, column cc (consecutive threads: columns)
+        const long long i = r0 + rr, j = c0 + cc;
+        double v = 0.0;
+        if (i < g.n && j < g.n) {
           double sq = 0.0;
           for (int k = 0; k < dim; ++k) {
             const double d = x[i * dim + k] - x[j * dim + k];
             sq = __builtin_fma(d, d, sq);
           }
-          kv = p.pv[o] * exp(-0.5 * sq / p.ls2[o]);
-          ko[i * ld + j] = kv;
-          ko[j * ld + i] = kv;
-        } else {
-          kv = ko[i * ld + j];
+          v = p.pv[o] * exp(-0.5 * sq / p.ls2[o]);
+          ko[i * ld + j] = v;                   // row i of the caller's matrix
         }
-        v = (p.scale_by_pv != 0.0 ? kv / p.pv[o] : kv) + (i == j ? p.jitter : 0.0);
-      } else {
-        v = (i == j) ? 1.0 : 0.0;
+        tile[rr][cc] = v;
       }
-    } else if (j < np_) {
-      const long long r = i - np_;
-      if (g.ident) v = (r == j && j < g.n) ? 1.0 : 0.0;
-      else v = (r == 0 && j < g.n) ? ycv[(long long)o * g.n + j] : 0.0;
+      __syncthreads();
+      if (ti != tj) {                           // the mirrored tile (rows j, columns i) from LDS
+        double* ko2 = km + (long long)o * ld * ld;
+        for (int e = tid; e < NB * NB; e += 256) {
+          const int rr = e >> 5, cc = e & 31;   // row c0 + rr, column r0 + cc
+          const long long i = c0 + rr, j = r0 + cc;
+          if (i < g.n && j < g.n) ko2[i * ld + j] = tile[cc][rr];
+        }
+      }
+    } else {
+      const double* ko = km + (long long)o * ld * ld;
+      bool asym = false;
+      for (int e = tid; e < NB * NB; e += 256) {
+        const int rr = e >> 5, cc = e & 31;
+        const long long i = r0 + rr, j = c0 + cc;
+        tile[rr][cc] = (i < g.n && j < g.n) ? ko[i * ld + j] : 0.0;
+      }
+      __syncthreads();
+      if (ti != tj) {                           // K[j][i] (the upper tile) against K[i][j]
+        for (int e = tid; e < NB * NB; e += 256) {
+          const int rr = e >> 5, cc = e & 31;   // K[c0 + rr][r0 + cc] vs tile[cc][rr]
+          const long long i = c0 + rr, j = r0 + cc;
+          if (i < g.n && j < g.n) {
+            const double u = ko[i * ld + j], l = tile[cc][rr];
+            asym = asym || !(u == l || (u != u && l != l));
+          }
+        }
+      } else {
+        for (int e = tid; e < NB * NB; e += 256) {
+          const int rr = e >> 5, cc = e & 31;
+          const long long i = r0 + rr, j = c0 + cc;
+          if (i < g.n && j < g.n && rr > cc) {
+            const double u = tile[cc][rr], l = tile[rr][cc];
+            asym = asym || !(u == l || (u != u && l != l));
+          }
+        }
+      }
+      if (asym) atomicOr(status + o, 2);
     }
+    __syncthreads();
+    const double scale = g.ident ? 1.0 : p.pv[o];
+#pragma unroll
+    for (int pass = 0; pass < NB / 8; ++pass) {
+      const int cc = c + 8 * pass;
+      const long long i = r0 + r, j = c0 + cc;
+      if (i < j) continue;
+      double v;
+      if (i < g.n && j < g.n) {
+        const double kv = tile[r][cc];
+        v = (g.ident ? kv : kv / scale) + (i == j ? p.jitter : 0.0);
+      } else {
+        v = i == j ? 1.0 : 0.0;
+      }
+      Ao[j * g.Na + i] = v;
+    }
+    return;
+  }
+  // bottom tiles
+#pragma unroll
+  for (int pass = 0; pass < NB / 8; ++pass) {
+    const int cc = c + 8 * pass;
+    const long long i = r0 + r, j = c0 + cc;
+    double v;
+    if (g.ident) v = (i - np_ == j && j < g.n) ? 1.0 : 0.0;
+    else v = (i == np_ && j < g.n) ? y[j * ld_y + o] - p.pm[o] : 0.0;
     Ao[j * g.Na + i] = v;
   }
 }
 
-// yc = (y - pm) / std(y - pm) per objective (population std; unscaled when 0),
-// numba_kernels.py:201-208.  One workgroup per objective.
-__global__ __launch_bounds__(1024) void ystd_kernel(double* __restrict__ ycv, const double* __restrict__ y,
-                                                    long long ld_y, int n, FitParams p) {
-  __shared__ double red[1024];
-  const int o = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
-  double* yc = ycv + (long long)o * n;
-  double s = 0.0;
-  for (int i = tid; i < n; i += nt) {
-    const double v = y[(long long)i * ld_y + o] - p.pm[o];
-    yc[i] = v;
-    s += v;
-  }
-  red[tid] = s;
-  __syncthreads();
-  for (int w = nt / 2; w > 0; w >>= 1) { if (tid < w) red[tid] += red[tid + w]; __syncthreads(); }
-  const double mean = red[0] / n;
-  __syncthreads();
-  s = 0.0;
-  for (int i = tid; i < n; i += nt) { const double d = yc[i] - mean; s += d * d; }
-  red[tid] = s;
-  __syncthreads();
-  for (int w = nt / 2; w > 0; w >>= 1) { if (tid < w) red[tid] += red[tid + w]; __syncthreads(); }
-  const double sd = sqrt(red[0] / n);
-  if (sd > 0.0)
-    for (int i = tid; i < n; i += nt) yc[i] = yc[i] / sd;
-}
-
-// ------------------------------------------------------------------------ panel
-// lane l's value of a wave-uniform broadcast (v_readlane on both halves)
-__device__ __forceinline__ double rdlane(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Row blocks of step k: [k, k+1, ..., nbt-1, nbt, ..., nbt+ra-1] (ra live bottom blocks).
-__device__ __forceinline__ int panel_row(int idx, int k, int nbt) {
-  return idx < nbt - k ? k + idx : nbt + (idx - (nbt - k));
-}
-
-// Step k, per objective (blockIdx.y), 4 row blocks per workgroup (one per wave):
-//   wave 0 factors the diagonal tile A_kk in LDS (lane r = row r, right-looking, column j of L
-//   broadcast through LDS; single wave, so no barrier between the columns);
-//   then wave w takes row block R[4 blockIdx.x + w]: the diagonal block writes L_kk, the others
-//   solve X L_kk^T = A_ik by row substitution (lane r = row r of the block).
-__global__ __launch_bounds__(256) void chol_panel_kernel(double* __restrict__ A, Aug g, int k, int n_rows,
-                                                        int* __restrict__ status) {
-  __shared__ double L[NB][NB + 1];
-  __shared__ double col[NB];
-  __shared__ double rdiag[NB];
-  const int o = blockIdx.y;
-  double* Ao = A + (long long)o * g.Na * g.Na;
+// ------------------------------------------------------------------------------- step
+// Panel role of launch k, one workgroup per (objective, slab block sb > k); wave 0 factors.
+__device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g, int o, int k, int w_slab,
+                                           double* __restrict__ part, int* __restrict__ status,
+                                           double* Cs, double* colb) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long long k0 = (long long)k * NB;
-  if (wave == 0) {
-    double a[NB];
-    const double* src = Ao + k0 * g.Na + k0 + lane;       // (k0 + lane, k0 + t) at src[t Na]
+  const int li = lane & 15, lg = lane >> 4;
+  const long long Na = g.Na;
+  const long long cK = (long long)k * NB;
+  const int sb = k + 1 + w_slab;
+  const int lr0 = 16 * wave;                                      // local rows: 0..31 diagonal, 32..63 slab
+  const long long grow0 = wave < 2 ? cK + lr0 : (long long)sb * NB + (lr0 - 32);
+  const int ntb = wave == 0 ? 1 : 2;                              // rows 0..15: t 16..31 are upper
+  d4 acc[2];
+  acc[0] = (d4){0.0, 0.0, 0.0, 0.0};
+  acc[1] = acc[0];
+  if (k > 0) {
+    // step k-1's update of this wave's 16 rows: D[t][r] = sum_s L(diag t, s) L(row r, s)
+    const double* Lp = Ao + (cK - NB) * Na;
+    double av[2][8], bv[8];
+    // bottom block k of the inverse is structurally zero in column block k-1 (never written)
+    const bool zero_rows = g.ident && wave >= 2 && sb == g.nbt + k;
 #pragma unroll
-    for (int t = 0; t < NB; ++t) a[t] = t <= lane ? src[t * g.Na] : 0.0;
-    // a[t > lane] is scratch: it only ever receives updates, never feeds a real entry
-    bool bad = false;
+    for (int ks = 0; ks < 8; ++ks) bv[ks] = zero_rows ? 0.0 : Lp[(4 * ks + lg) * Na + grow0 + li];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const double piv = rdlane(a[j], j);
-      bad = bad || !(piv > 0.0);             // potrf: ajj <= 0 or NaN -> not positive definite
-      const double d = sqrt(piv);
-      const double rd = 1.0 / d;               // wave-uniform: one reciprocal per column
-      const double lj = lane == j ? d : (lane > j ? a[j] * rd : 0.0);
-      a[j] = lj;
-      col[lane] = lj;
-      if (lane == 0) rdiag[j] = rd;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
-      for (int t = j + 1; t < NB; ++t) a[t] = __builtin_fma(-lj, col[t], a[t]);
-      __builtin_amdgcn_wave_barrier();
+      for (int ks = 0; ks < 8; ++ks)
+        av[tb][ks] = tb < ntb ? Lp[(4 * ks + lg) * Na + cK + 16 * tb + li] : 0.0;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      acc[0] = mfma64(av[0][ks], bv[ks], acc[0]);
+      if (ntb > 1) acc[1] = mfma64(av[1][ks], bv[ks], acc[1]);
     }
-#pragma unroll
-    for (int t = 0; t < NB; ++t) L[lane][t] = a[t];
-    // identity padding and the never-factored bottom rows cannot fail: any bad pivot is real
-    if (bad && blockIdx.x == 0 && lane == 0) atomicOr(status + o, 1);
   }
+  // C = A - D into LDS, row-major [local row][t]; diagonal rows' upper entries zeroed
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 16 * tb + lg + 4 * i;
+      const int rl = lr0 + li;
+      double v = 0.0;
+      if (tb < ntb && !(wave < 2 && rl < t)) v = Ao[(cK + t) * Na + grow0 + li] - acc[tb][i];
+      Cs[rl * CS + t] = v;
+    }
   __syncthreads();
-  const int idx = 4 * blockIdx.x + wave;
-  if (idx >= n_rows) return;
-  const long long i0 = (long long)panel_row(idx, k, g.nbt) * NB;
-  double* dst = Ao + k0 * g.Na + i0 + lane;              // (i0 + lane, k0 + t) at dst[t Na]
-  if (idx == 0) {
+  if (wave != 0) return;
+  double a[NB];
 #pragma unroll
-    for (int t = 0; t < NB; ++t)
-      if (t <= lane) dst[t * g.Na] = L[lane][t];
-    return;
-  }
-  // x L_kk^T = a:  x_j = (a_j - sum_{t<j} x_t L_jt) / L_jj   (two partial sums for ILP; the
-  // division as a product with the reciprocal the factorisation computed)
-  double x[NB];
-#pragma unroll
-  for (int t = 0; t < NB; ++t) x[t] = dst[t * g.Na];
+  for (int t = 0; t < NB; ++t) a[t] = Cs[lane * CS + t];
+  double dj = 1.0;
+  bool bad = false;
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    double s0 = x[j], s1 = 0.0;
+    const double piv = bo_readlane_d(a[j], j);
+    bad = bad || !(piv > 0.0);                                   // potrf: a_jj <= 0 or NaN
+    const double rs = rsqrt_nr(piv);
+    const double d = piv * rs;
+    a[j] = lane == j ? d : a[j] * rs;                           // lanes > j: L_ij; lanes < j: unused
+    dj = lane == j ? d : dj;
+    if (j + 1 < NB) {
+      const double l1 = bo_readlane_d(a[j], j + 1);             // L(j+1, j): the next pivot first
+      a[j + 1] = __builtin_fma(-a[j], l1, a[j + 1]);
+      if (j + 2 < NB) {
+        if (lane < NB) colb[j * NB + lane] = a[j];
+        wave_lds_sync();
 #pragma unroll
-    for (int t = 0; t < j; ++t) {
-      if (t & 1) s1 = __builtin_fma(-x[t], L[j][t], s1);
-      else s0 = __builtin_fma(-x[t], L[j][t], s0);
+        for (int t = j + 2; t < NB; ++t) a[t] = __builtin_fma(-a[j], colb[j * NB + t], a[t]);
+      }
     }
-    x[j] = (s0 + s1) * rdiag[j];
+  }
+  // L_kk (one workgroup writes it) and the slab's L rows
+  if (w_slab == 0) {
+#pragma unroll
+    for (int t = 0; t < NB; ++t)
+      if (lane < NB && t <= lane) Ao[(cK + t) * Na + cK + lane] = a[t];
   }
 #pragma unroll
-  for (int t = 0; t < NB; ++t) dst[t * g.Na] = x[t];
-}
-
-// ----------------------------------------------------------------------- update
-__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-// triangular index t -> (i, j), j <= i, t = i (i + 1) / 2 + j
-__device__ __forceinline__ void tri_decode(long long t, int& i, int& j) {
-  int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-  while ((long long)(r + 1) * (r + 2) / 2 <= t) ++r;
-  while ((long long)r * (r + 1) / 2 > t) --r;
-  i = r;
-  j = (int)(t - (long long)r * (r + 1) / 2);
-}
-
-// Trailing update of step k: A_pq -= L_pk L_qk^T for every live tile, k < q <= p:
-//   T1 top x top (m (m + 1) / 2), T2 bottom x top (ra m), T3 bottom x bottom (ra (ra + 1) / 2),
-//   m = nbt - k - 1.  L_pk and L_qk are staged in LDS transposed (PT[c][r], stride 66, from
-//   coalesced column-major loads); the MFMAs compute C^T = L_qk L_pk^T so that a lane's output
-//   rows are consecutive rows of the column-major A: wave w takes q-rows 16 w .. 16 w + 15 of
-//   the tile against 4 blocks of 16 p-rows, over 16 k-steps.
-__global__ __launch_bounds__(256) void chol_update_kernel(double* __restrict__ A, Aug g, int k, int ra) {
-  extern __shared__ double lds[];
-  double* P = lds;
-  double* Q = lds + NB * LS;
-  const int o = blockIdx.y;
-  double* Ao = A + (long long)o * g.Na * g.Na;
-  const int m = g.nbt - k - 1;
-  const long long T1 = (long long)m * (m + 1) / 2, T2 = (long long)ra * m;
-  long long t = blockIdx.x;
-  int p, q;
-  if (t < T1) {
-    int i, j;
-    tri_decode(t, i, j);
-    p = k + 1 + i;
-    q = k + 1 + j;
-  } else if (t < T1 + T2) {
-    t -= T1;
-    p = g.nbt + (int)(t / m);
-    q = k + 1 + (int)(t % m);
-  } else {
-    int i, j;
-    tri_decode(t - T1 - T2, i, j);
-    p = g.nbt + i;
-    q = g.nbt + j;
+  for (int t = 0; t < NB; ++t)
+    if (lane >= NB) Ao[(cK + t) * Na + (long long)sb * NB + lane - NB] = a[t];
+  if (g.ident) {
+    if (w_slab == 0 && bad && lane == 0) atomicOr(status + o, 1);
+    return;
   }
-  const long long k0 = (long long)k * NB, p0 = (long long)p * NB, q0 = (long long)q * NB;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int e = tid; e < NB * NB; e += 256) {
-    const int r = e & 63, c = e >> 6;                     // (row r, column c) of the tiles
-    P[c * LS + r] = Ao[(k0 + c) * g.Na + p0 + r];
-    Q[c * LS + r] = Ao[(k0 + c) * g.Na + q0 + r];
-  }
-  __syncthreads();
-  d4 acc[4];
+  if (w_slab == 0) {
+    double v = (lane < NB && cK + lane < g.n) ? log(dj) : 0.0;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) acc[b] = (d4){0.0, 0.0, 0.0, 0.0};
-  const int arow = 16 * wave + (lane & 15), ca = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < NB / 4; ++s) {
-    const double av = Q[(4 * s + ca) * LS + arow];        // A = L_qk rows 16 w ..
-#pragma unroll
-    for (int b = 0; b < 4; ++b)                           // B = L_pk^T, p-rows 16 b ..
-      acc[b] = mfma64(av, P[(4 * s + ca) * LS + 16 * b + (lane & 15)], acc[b]);
-  }
-  // D[(l >> 4) + 4 r][l & 15] of block (wave, b): q-row 16 wave + (l >> 4) + 4 r, p-row
-  // 16 b + (l & 15), i.e. element (p0 + p-row, q0 + q-row) of A, column-major
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      double* c = Ao + (q0 + 16 * wave + (lane >> 4) + 4 * r) * g.Na + p0 + 16 * b + (lane & 15);
-      *c -= acc[b][r];
+    for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+    if (lane == 0) {
+      part[(long long)o * part_len(g) + k] = v;
+      if (bad) atomicOr(status + o, 1);
     }
-}
-
-// ------------------------------------------------------------------------ finish
-// mll[o] = -0.5 yc . alpha - 0.5 log det - 0.5 N log(2 pi)   (numba_kernels.py:222-232):
-// yc . alpha = |z|^2 = -(corner), log det = 2 sum_{i<N} log L_ii.
-__global__ __launch_bounds__(1024) void mll_finish_kernel(const double* __restrict__ A, Aug g,
-                                                          double* __restrict__ mll) {
-  __shared__ double red[1024];
-  const int o = blockIdx.x, tid = threadIdx.x;
-  const double* Ao = A + (long long)o * g.Na * g.Na;
-  double s = 0.0;
-  for (int i = tid; i < g.n; i += blockDim.x) s += log(Ao[(long long)i * g.Na + i]);
-  red[tid] = s;
-  __syncthreads();
-  for (int w = blockDim.x / 2; w > 0; w >>= 1) { if (tid < w) red[tid] += red[tid + w]; __syncthreads(); }
-  if (tid == 0) {
-    const long long c = (long long)g.nbt * NB;
-    const double fit = -Ao[c * g.Na + c];
-    const double logdet = 2.0 * red[0];
-    mll[o] = -0.5 * fit + (-0.5 * logdet) + (-0.5 * g.n * log(2.0 * 3.141592653589793));
+  }
+  if (sb == g.nbt && lane == NB) {                               // the bottom row z = L^-1 (y - pm)
+    double s = 0.0;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) s = __builtin_fma(a[t], a[t], s);
+    part[(long long)o * part_len(g) + g.nbt + k] = s;
   }
 }
 
-// out[o][i][j] = -A[n_p + i][n_p + j] (lower), mirrored: the symmetric K^-1.
-__global__ void inv_finish_kernel(double* __restrict__ out, const double* __restrict__ A, Aug g,
-                                  const int* __restrict__ status) {
-  const int o = blockIdx.y;
-  if (status[o]) return;                       // this objective goes through the LU fallback
+// L part (MLL and inverse): the column blocks c = k+1 .. nbt-1, each with its row blocks
+// [c, RB); numbered from the last column, whose count is `base`:  S(u) = u base + u (u - 1) / 2.
+__device__ __forceinline__ long long lpart_S(long long u, long long base) { return u * base + u * (u - 1) / 2; }
+
+// Update role of launch k (step s = k - 1): one 32 x 32 tile per wave.
+__device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g, int k, long long TL,
+                                            long long TC, long long wt) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+  const long long per = TL + TC;
+  if (wt >= per * g.n_obj) return;
+  const int o = (int)(wt / per);
+  long long t = wt % per;
   const long long np_ = (long long)g.nbt * NB;
-  const double* Ao = A + (long long)o * g.Na * g.Na;
+  long long row0, col0;
+  bool first = false;
+  if (t < TL) {
+    const long long base = g.ident ? k + 1 : 2;
+    const double bb = 2.0 * (double)base - 1.0;
+    long long u = (long long)((-bb + sqrt(bb * bb + 8.0 * (double)t)) * 0.5);
+    if (u < 0) u = 0;
+    while (lpart_S(u + 1, base) <= t) ++u;
+    while (lpart_S(u, base) > t) --u;
+    const long long c = g.nbt - 1 - u;
+    row0 = (c + (t - lpart_S(u, base))) * NB;
+    col0 = c * NB;
+  } else {
+    t -= TL;
+    const int u = tri_row(t);
+    const long long cp = k - 1 - u;
+    const long long b = cp + (t - (long long)u * (u + 1) / 2);
+    row0 = np_ + b * NB;
+    col0 = np_ + cp * NB;
+    first = b == k - 1;                          // C tile (b, cp): first contribution at step b
+  }
+  double* Ao = A + (long long)o * g.ostride;
+  const long long Na = g.Na;
+  const double* Lp = Ao + (long long)(k - 1) * NB * Na;
+  double av[2][8], bv[2][8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      av[h][ks] = Lp[(4 * ks + lg) * Na + col0 + 16 * h + li];
+      bv[h][ks] = Lp[(4 * ks + lg) * Na + row0 + 16 * h + li];
+    }
+  d4 acc[2][2];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = mfma64(av[tb][ks], bv[rb][ks], acc[tb][rb]);
+  // D[t][r]: t = 16 tb + lg + 4 i (tile column), r = 16 rb + li (tile row)
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double* c = Ao + (col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li;
+        *c = (first ? 0.0 : *c) - acc[tb][rb][i];
+      }
+}
+
+// Launch k: blocks [0, n_obj * n_panel) panel role, the rest update role (4 tiles per block).
+__global__ __launch_bounds__(256) void fit_step_kernel(double* __restrict__ A, Geo g, int k, int n_panel,
+                                                       long long TL, long long TC,
+                                                       double* __restrict__ part, int* __restrict__ status) {
+  __shared__ double Cs[2 * NB * CS];
+  __shared__ double colb[NB * NB];
+  const int np = g.n_obj * n_panel;
+  if ((int)blockIdx.x < np) {
+    const int o = blockIdx.x / n_panel;
+    panel_role(A + (long long)o * g.ostride, g, o, k, blockIdx.x % n_panel, part, status, Cs, colb);
+  } else {
+    update_role(A, g, k, TL, TC, ((long long)blockIdx.x - np) * 4 + (threadIdx.x >> 6));
+  }
+}
+
+// ---------------------------------------------------------------------------- finish
+// out[o][i][j] = -C[max(i, j)][min(i, j)] (C = the bottom-right block, lower triangle): the
+// symmetric K^-1.  32 x 32 output tiles: lower tiles read C column-major (coalesced), upper tiles
+// the mirrored lower tile through LDS; writes are row-major.
+__global__ __launch_bounds__(256) void inv_extract_kernel(double* __restrict__ out, const double* __restrict__ A,
+                                                          Geo g, const int* __restrict__ status) {
+  __shared__ double tile[NB][NB + 1];
+  const int o = blockIdx.z;
+  if (status[o]) return;                        // this objective goes through the LU path
+  const int bi = blockIdx.y, bj = blockIdx.x;   // output tile (rows 32 bi, columns 32 bj)
+  const long long np_ = (long long)g.nbt * NB;
+  const double* Ao = A + (long long)o * g.ostride;
   const long long n = g.n;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n * n;
-       t += (long long)gridDim.x * blockDim.x) {
-    const long long i = t / n, j = t - i * n;
-    const long long r = i >= j ? i : j, c = i >= j ? j : i;
-    out[(long long)o * n * n + t] = -Ao[(np_ + c) * g.Na + np_ + r];
+  const int lo = bi >= bj ? bi : bj, hi = bi >= bj ? bj : bi;   // source lower tile (lo, hi)
+  const int tid = threadIdx.x, c = tid >> 5, r = tid & 31;
+  // tile[cc][rr] = C(32 lo + rr, 32 hi + cc): column-major reads (rr consecutive)
+#pragma unroll
+  for (int pass = 0; pass < NB / 8; ++pass) {
+    const int cc = c + 8 * pass;
+    tile[cc][r] = Ao[(np_ + (long long)hi * NB + cc) * g.Na + np_ + (long long)lo * NB + r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int pass = 0; pass < NB / 8; ++pass) {
+    const int rr = c + 8 * pass;                 // output row 32 bi + rr, column 32 bj + r
+    const long long i = (long long)bi * NB + rr, j = (long long)bj * NB + r;
+    if (i >= n || j >= n) continue;
+    // element (i, j): lower (i >= j) -> C(i, j) = tile[j - 32 hi][i - 32 lo] with lo = bi
+    const long long gr = i >= j ? i : j, gc = i >= j ? j : i;
+    const double v = tile[gc - (long long)hi * NB][gr - (long long)lo * NB];
+    out[(long long)o * n * n + i * n + j] = -v;
   }
 }
 
@@ -422,39 +556,63 @@ __global__ void gather_cols_kernel(double* __restrict__ out, const double* __res
 
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-Aug make_aug(int n, bool ident) {
-  Aug g;
+Geo make_geo(int n, int n_obj, bool ident) {
+  Geo g;
   g.n = n;
   g.nbt = (n + NB - 1) / NB;
-  g.rb = ident ? g.nbt : 1;
   g.ident = ident ? 1 : 0;
-  g.Na = (long long)(g.nbt + g.rb) * NB;
+  g.n_obj = n_obj;
+  const long long np_ = (long long)g.nbt * NB;
+  g.Na = ident ? 2 * np_ : np_ + NB;
+  g.ncols = ident ? 2 * np_ : np_;
+  g.ostride = g.Na * g.ncols;
   return g;
 }
 
-// Blocked Cholesky of the first nbt tile columns of every objective's augmented matrix.
-int aug_factor(double* A, const Aug& g, int n_obj, int* status, hipStream_t s) {
-  static bool attr = false;
-  const size_t lds = 2 * NB * LS * sizeof(double);
-  if (!attr) {
-    BO_CHECK_HIP(hipFuncSetAttribute((const void*)chol_update_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  for (int k = 0; k < g.nbt; ++k) {
-    const int ra = g.ident ? (k + 1 < g.rb ? k + 1 : g.rb) : g.rb;
-    const int m = g.nbt - k - 1;
-    const int rows = 1 + m + ra;
-    hipLaunchKernelGGL(chol_panel_kernel, dim3((rows + 3) / 4, n_obj), dim3(256), 0, s, A, g, k, rows,
-                       status);
-    const long long tiles = (long long)m * (m + 1) / 2 + (long long)ra * m + (long long)ra * (ra + 1) / 2;
-    if (tiles > 0)
-      hipLaunchKernelGGL(chol_update_kernel, dim3((unsigned)tiles, n_obj), dim3(256), lds, s, A, g, k, ra);
+size_t geo_bytes(const Geo& g) { return a256((size_t)g.n_obj * g.ostride * sizeof(double)); }
+
+// init launch + one launch per step (inverse: one more, the last step's update of C)
+int fit_factor(double* A, const Geo& g, const double* km, long long ld, const double* x, int dim,
+               const double* y, long long ld_y, const FitParams& p, double* part, int* status,
+               hipStream_t s) {
+  const long long tri = (long long)g.nbt * (g.nbt + 1) / 2;
+  const long long tiles = g.ident ? 2 * tri : tri + g.nbt;
+  const long long blocks = g.n_obj * tiles + (g.ident ? 0 : g.n_obj);
+  hipLaunchKernelGGL(fit_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s, A, g, (double*)km, ld,
+                     x, dim, y, ld_y, p, part, status, (int)tiles);
+  BO_CHECK_HIP(hipGetLastError());
+  const int steps = g.ident ? g.nbt + 1 : g.nbt;
+  for (int k = 0; k < steps; ++k) {
+    const int n_panel = k < g.nbt ? (g.ident ? g.nbt : g.nbt - k) : 0;
+    long long TL = 0, TC = 0;
+    if (k >= 1) {
+      const long long m = g.nbt - 1 - k;
+      const long long base = g.ident ? k + 1 : 2;
+      TL = m > 0 ? m * base + m * (m - 1) / 2 : 0;
+      TC = g.ident ? (long long)k * (k + 1) / 2 : 0;
+    }
+    const long long upd = ((TL + TC) * g.n_obj + 3) / 4;
+    const long long grid = (long long)g.n_obj * n_panel + upd;
+    if (grid == 0) continue;
+    hipLaunchKernelGGL(fit_step_kernel, dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
+                       part, status);
   }
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
 }
 
-size_t aug_bytes(int n_obj, const Aug& g) { return a256((size_t)n_obj * g.Na * g.Na * sizeof(double)); }
+// pinned staging for the per-call read-back (one per host thread)
+void* pinned(size_t bytes) {
+  thread_local void* buf = nullptr;
+  thread_local size_t cap = 0;
+  if (cap < bytes) {
+    if (buf) (void)hipHostFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (hipHostMalloc(&buf, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    cap = bytes;
+  }
+  return buf;
+}
 
 }  // namespace
 
@@ -462,9 +620,9 @@ extern "C" {
 
 size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n) {
   if (n_obj < 1 || n < 1) return 0;
-  const Aug g = make_aug((int)n, true);
+  const Geo g = make_geo((int)n, n_obj, true);
   const size_t lu = 2 * a256((size_t)n * n * sizeof(double)) + 2 * a256((size_t)n * sizeof(int));
-  return aug_bytes(n_obj, g) + lu + 512;
+  return geo_bytes(g) + lu + 512;
 }
 
 int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_t n, void* ws,
@@ -473,10 +631,10 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
   if (n > (1 << 15)) return BO_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < bo_invert_k_workspace_size(n_obj, n)) return BO_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
-  const Aug g = make_aug((int)n, true);
+  const Geo g = make_geo((int)n, n_obj, true);
   char* w = (char*)ws;
   double* A = (double*)w;
-  char* lu = w + aug_bytes(n_obj, g);
+  char* lu = w + geo_bytes(g);
   double* bufA = (double*)lu;
   double* bufB = (double*)(lu + a256((size_t)n * n * sizeof(double)));
   int* piv = (int*)(lu + 2 * a256((size_t)n * n * sizeof(double)));
@@ -486,19 +644,20 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
   FitParams p;
   memset(&p, 0, sizeof(p));
   p.jitter = BO_KERNEL_JITTER;                 // numba_kernels.py:397-398
-  hipLaunchKernelGGL(aug_init_kernel, dim3((unsigned)g.Na, n_obj), dim3(256), 0, s, A, g,
-                     (double*)km, (long long)ld, (const double*)nullptr, 0, (const double*)nullptr, p, 0);
-  BO_CHECK_HIP(hipGetLastError());
-  int st = aug_factor(A, g, n_obj, status, s);
+  int st = fit_factor(A, g, km, ld, nullptr, 0, nullptr, 0, p, nullptr, status, s);
   if (st != BO_OK) return st;
-  hipLaunchKernelGGL(inv_finish_kernel, dim3(1024, n_obj), dim3(256), 0, s, out, A, g, status);
+  const unsigned nt = (unsigned)g.nbt;
+  hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, n_obj), dim3(256), 0, s, out, A, g, status);
   BO_CHECK_HIP(hipGetLastError());
-  int hstat[BO_MAX_OBJ + 1];
+  int* hstat = (int*)pinned(sizeof(int) * BO_MAX_OBJ);
+  if (!hstat) return BO_ERR_HIP;
   BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * n_obj, hipMemcpyDeviceToHost, s));
   BO_CHECK_HIP(hipStreamSynchronize(s));
+  int fail[BO_MAX_OBJ];
+  for (int o = 0; o < n_obj; ++o) fail[o] = hstat[o];
   // LU fallback (Gauss-Jordan, partial pivoting) for the objectives whose Cholesky failed
   for (int o = 0; o < n_obj; ++o) {
-    if (!hstat[o]) continue;
+    if (!fail[o]) continue;
     int* gstat = status + BO_MAX_OBJ + 1;
     BO_CHECK_HIP(hipMemsetAsync(gstat, 0, sizeof(int), s));
     const long long total = (long long)n * n;
@@ -542,9 +701,8 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
 
 size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n) {
   if (n_obj < 1 || n < 1) return 0;
-  const Aug g = make_aug((int)n, false);
-  return aug_bytes(n_obj, g) + a256((size_t)n_obj * n * sizeof(double)) +
-         a256((size_t)BO_MAX_OBJ * sizeof(double)) + 512;
+  const Geo g = make_geo((int)n, n_obj, false);
+  return geo_bytes(g) + a256((size_t)n_obj * part_len(g) * sizeof(double) + BO_MAX_OBJ * sizeof(int)) + 512;
 }
 
 int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* y, int64_t ld_y,
@@ -556,12 +714,10 @@ int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* 
   if (n > (1 << 16)) return BO_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < bo_compute_mll_workspace_size(n_obj, n)) return BO_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
-  const Aug g = make_aug((int)n, false);
-  char* w = (char*)ws;
-  double* A = (double*)w;
-  double* ycv = (double*)(w + aug_bytes(n_obj, g));
-  double* dmll = (double*)((char*)ycv + a256((size_t)n_obj * n * sizeof(double)));
-  int* status = (int*)((char*)dmll + a256((size_t)BO_MAX_OBJ * sizeof(double)));
+  const Geo g = make_geo((int)n, n_obj, false);
+  double* A = (double*)ws;
+  double* part = (double*)((char*)ws + geo_bytes(g));
+  int* status = (int*)(part + (size_t)n_obj * part_len(g));
   FitParams p;
   memset(&p, 0, sizeof(p));
   for (int o = 0; o < n_obj; ++o) {
@@ -570,26 +726,31 @@ int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* 
     p.ls2[o] = ls[o] * ls[o];
   }
   p.jitter = BO_CHOLESKY_JITTER;               // numba_kernels.py:211-214
-  p.scale_by_pv = 1.0;                         // correlation matrix K / pv (:195-198)
-  BO_CHECK_HIP(hipMemsetAsync(status, 0, 256, s));
-  hipLaunchKernelGGL(ystd_kernel, dim3(n_obj), dim3(1024), 0, s, ycv, y, (long long)ld_y, (int)n, p);
-  hipLaunchKernelGGL(aug_init_kernel, dim3((unsigned)g.Na, n_obj), dim3(256), 0, s, A, g, km,
-                     (long long)ld, x, dim, ycv, p, 1);
-  BO_CHECK_HIP(hipGetLastError());
-  int st = aug_factor(A, g, n_obj, status, s);
+  BO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * n_obj, s));
+  int st = fit_factor(A, g, km, ld, x, dim, y, ld_y, p, part, status, s);
   if (st != BO_OK) return st;
-  hipLaunchKernelGGL(mll_finish_kernel, dim3(n_obj), dim3(1024), 0, s, A, g, dmll);
-  BO_CHECK_HIP(hipGetLastError());
-  double h[BO_MAX_OBJ];
-  int hstat[BO_MAX_OBJ];
-  BO_CHECK_HIP(hipMemcpyAsync(h, dmll, sizeof(double) * n_obj, hipMemcpyDeviceToHost, s));
-  BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * n_obj, hipMemcpyDeviceToHost, s));
+  const size_t bytes = (size_t)n_obj * part_len(g) * sizeof(double) + sizeof(int) * n_obj;
+  double* h = (double*)pinned(bytes);
+  if (!h) return BO_ERR_HIP;
+  BO_CHECK_HIP(hipMemcpyAsync(h, part, bytes, hipMemcpyDeviceToHost, s));
   BO_CHECK_HIP(hipStreamSynchronize(s));
+  const int* hstat = (const int*)(h + (size_t)n_obj * part_len(g));
   for (int o = 0; o < n_obj; ++o)
     if (hstat[o]) return BO_ERR_NOT_PD;
-  // np.sum over objectives (numba_kernels.py:235): sequential for fewer than 8 terms
+  // mll_o = -0.5 yc.alpha - 0.5 log det - 0.5 N log(2 pi) (numba_kernels.py:222-232); yc.alpha =
+  // |z|^2 / var(y - pm) (unscaled when the std is 0, :206-207); np.sum over objectives (:235)
   double tot = 0.0;
-  for (int o = 0; o < n_obj; ++o) tot += h[o];
+  for (int o = 0; o < n_obj; ++o) {
+    const double* q = h + (size_t)o * part_len(g);
+    double ld_sum = 0.0, fit = 0.0;
+    for (int k = 0; k < g.nbt; ++k) {
+      ld_sum += q[k];
+      fit += q[g.nbt + k];
+    }
+    const double var = q[2 * g.nbt];
+    if (sqrt(var) > 0.0) fit /= var;
+    tot += -0.5 * fit + (-0.5 * (2.0 * ld_sum)) + (-0.5 * (double)n * log(2.0 * 3.141592653589793));
+  }
   *mll_out = tot;
   return BO_OK;
 }

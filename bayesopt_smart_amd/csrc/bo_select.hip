@@ -114,6 +114,7 @@ struct SelArgs {
   const int* hidx;
   unsigned int hmask;
   TopEntry* partial;
+  long long partial_cap;    // entries of `partial` (the debug build checks every write)
   SobolArgs sob;            // kind BO_CAND_SOBOL
 };
 
@@ -147,7 +148,7 @@ __device__ __forceinline__ bool cand_excluded(const SelArgs& a, long long j,
 #pragma unroll
     for (int k = 0; k < BO_MAX_DIM; ++k) c[k] = k < a.dim ? cand_coord(a, j, k) : 0.0;
   }
-  if (hk) return bo_hash_contains(hk, hi, hm, a.excl, a.dim, c, a.dim);
+  if (hk) return bo_hash_contains(hk, hi, hm, a.excl, a.dim, c, a.dim, a.n_excl);
   for (int e = 0; e < a.n_excl; ++e) {
     bool eq = true;
 #pragma unroll
@@ -226,8 +227,8 @@ __device__ __forceinline__ void wave_rank_insert(double& lv, long long& li, doub
   for (int l = 0; l < q; ++l)
     rn += bo_key_before(bo_readlane_u(kl, l), bo_readlane_i(li, l), kn, ni) ? 1 : 0;
   wave_lds_sync();
-  if (lane < q && rl < q) { buf[rl].v = lv; buf[rl].i = li; }
-  if (pass && rn < q) { buf[rn].v = nv; buf[rn].i = ni; }
+  if (lane < q && rl < q && BO_IN(rl, 64, "rank insert buf[rl]")) { buf[rl].v = lv; buf[rl].i = li; }
+  if (pass && rn < q && BO_IN(rn, 64, "rank insert buf[rn]")) { buf[rn].v = nv; buf[rn].i = ni; }
   wave_lds_sync();
   if (lane < q) { lv = buf[lane].v; li = buf[lane].i; }
 }
@@ -262,6 +263,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
       const unsigned long long key = bo_point_key(a.excl + (long long)e * a.dim, a.dim);
       if (key != 0ull) bo_hash_insert(lkeys, lidx, (unsigned int)a.lds_slots - 1, key, e);
     }
+    if (!BO_IN(a.n_excl, a.lds_slots / 2 + 1, "LDS hash load")) return;
     __syncthreads();
     hk = lkeys;
     hi = lidx;
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
         wave_lds_sync();
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (take[u] && off[u] >= c0 && off[u] < c0 + 64) {
+          if (take[u] && off[u] >= c0 && off[u] < c0 + 64 && BO_IN(off[u] - c0, 64, "chunk buf[off - c0]")) {
             buf[off[u] - c0].v = val[u];
             buf[off[u] - c0].i = a.cand_offset + b0 + u * stride + lane;
           }
@@ -359,7 +361,8 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
         const double nv = p ? buf[lane].v : -__builtin_inf();
         const long long ni = p ? buf[lane].i : -1;
         p = p && bo_better(nv, ni, tv, ti);
-        if (a.n_excl > 0 && p) p = !cand_excluded(a, ni - a.cand_offset, hk, hi, hm);
+        if (a.n_excl > 0 && p && BO_IN(ni - a.cand_offset, a.n_cand, "chunk candidate"))
+          p = !cand_excluded(a, ni - a.cand_offset, hk, hi, hm);
         if (__ballot(p) == 0ull) continue;
         if (bo_readlane_i(li, 0) < 0 && __popcll(__ballot(p)) > 24) {
           // empty list and a large chunk: the sorted chunk's head is the list (rank insertion
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
       }
     }
   }
-  if (lane < q) {
+  if (lane < q && BO_IN(((long long)blockIdx.x * 4 + wave) * q + lane, a.partial_cap, "partial list entry")) {
     TopEntry* dst = a.partial + ((size_t)blockIdx.x * 4 + wave) * q;
     dst[lane].v = lv;
     dst[lane].i = li;
@@ -579,6 +582,7 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
     }
   a.excl = excl;
   a.partial = (TopEntry*)ws;
+  a.partial_cap = (long long)(sel_lists_bytes(topq) / sizeof(TopEntry));
   if (n_excl > 0 && n_cand > 0) {
     // the evaluated points' hash set: per workgroup in LDS (<= 1024 points),
     // else in the workspace region after the lists when it fits (2 n_excl .. 4 n_excl slots of

@@ -23,7 +23,8 @@ def require_device(device=None):
     dev = torch.device(device)
     if dev.type != "cuda":
         raise RuntimeError(f"bayesopt_smart_amd tensors must live on a HIP device, got {dev}")
-    return dev
+    # always an indexed device ('cuda' -> 'cuda:<current>'), so that device checks compare equal
+    return dev if dev.index is not None else torch.device("cuda", torch.cuda.current_device())
 
 
 def stream_handle(device=None):

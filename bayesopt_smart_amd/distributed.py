@@ -98,11 +98,15 @@ def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_var
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     off, cnt = shard_range(cands.n, rank, world)
     score = scorer or predict_acquire
-    kw = {} if scorer is not None else {"device": device}
+    if scorer is None:
+        from .device import require_device
+        dev = require_device(device)              # indexed: 'cuda' -> 'cuda:<current>'
+        kw = {"device": dev}
+    else:
+        dev = torch.device("cpu")
+        kw = {}
     if q > 0:
-        dev = torch.device("cpu") if scorer is not None else device
-        kw["top_rec"] = torch.empty(2 * q, dtype=torch.float64,
-                                    device=dev if dev is not None else torch.device("cuda", torch.cuda.current_device()))
+        kw["top_rec"] = torch.empty(2 * q, dtype=torch.float64, device=dev)
     r = score(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales, betas,
               outputs=outputs, topq=q, offset=off, count=cnt, **kw)
     if world == 1:

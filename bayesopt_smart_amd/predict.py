@@ -252,7 +252,9 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
     if nbytes == 0:
         raise _lib.BoNativeError(_lib.ERR_ARG, "bo_predict_workspace_size")
     ws = Workspace.get(nbytes, dev)
-    res["_keepalive"] = (x_train, y_train, kinv, excl_points)
+    # every raw pointer the descriptor (or a graph captured from it) holds must stay owned: the
+    # inputs, the candidate set (its tensor, or the host Sobol descriptor read during the call)
+    res["_keepalive"] = (x_train, y_train, kinv, excl_points, cands, cands.tensor, cands.sobol)
     call = PreparedPredict(lib, desc, ws, stream_handle(dev), res, dev)
     return call if prepare else call()
 
@@ -296,6 +298,9 @@ class PreparedPredict:
             g.replay()
             return res
         replay.graph = g
+        # the graph bakes in the workspace pointer (packed W, partial lists) and the descriptor's
+        # pointers: the replay owns this call (and through it the workspace tensor and res)
+        replay.prepared = self
         return replay
 
 

@@ -225,8 +225,8 @@ int bo_pareto_mask(const double* y, int64_t n, int32_t n_obj, uint8_t* mask, voi
  * mu + beta sigma in objective units).  boxes: device copy of bo_hvi_boxes' output.  NaN in p
  * gives NaN (selected first, as NaN is by the reference's argsort).  shift/scale host. */
 /* bo_hvi_select_topq: the exact HVI of bo_hypervolume_improvement_exact written into acq AND
- * the top-q selection of bo_select_topq over it, in one pass over the UCB arrays (q <= 16;
- * larger q runs the two steps).  Arguments as those two functions'; workspace
+ * the top-q selection of bo_select_topq over it, in one pass over the UCB arrays, any
+ * q <= BO_MAX_TOPQ, n_obj <= 4.  Arguments as those two functions'; workspace
  * bo_select_topq_workspace_size(n_cand, topq). */
 int bo_hvi_select_topq(double* acq, const double* ucb, int64_t ld, int64_t n_cand, int32_t n_obj,
                        const double* shift, const double* scale, const double* boxes,

@@ -1,9 +1,13 @@
-"""CPU model of the device fit's tile schedule (bayesopt_smart_amd/csrc/bo_fit.hip): the
-right-looking blocked Cholesky of the AUGMENTED matrix [[K, .], [B, C]], with exactly the panel
-row blocks and trailing-update tiles the kernels launch per step (including the skipped
-structurally-zero tiles of the inverse), reproduces compute_mll (numba_kernels.py:152-235) and
-invert_k (:370-403).  Runs in numpy with small tiles so that every branch of the schedule
-(several steps, padding, ragged N) is exercised; the GPU tests check the kernels themselves."""
+"""CPU model of the device fit's launch schedule (bayesopt_smart_amd/csrc/bo_fit.hip): the
+right-looking blocked Cholesky of the AUGMENTED matrix [[K, .], [B, C]] with one launch per
+column step, each launch running the panel of step k (with step k-1's update of its own column
+block, lookahead) beside step k-1's update of every other live tile -- exactly the panel slabs,
+the update tiles (decoded from the linear task index as update_role decodes them) and the
+structurally-zero tiles the kernels skip.  Reproduces compute_mll (numba_kernels.py:152-235) and
+invert_k (:370-403).  Runs in numpy with small tiles so that every branch of the schedule (several
+steps, padding, ragged N) is exercised; the GPU tests check the kernels themselves."""
+
+import math
 
 import numpy as np
 import pytest
@@ -11,78 +15,132 @@ import pytest
 from oracle import oracle_np as O
 
 
-def _tri(t):
-    i = int((np.sqrt(8.0 * t + 1.0) - 1.0) * 0.5)
-    while (i + 1) * (i + 2) // 2 <= t:
-        i += 1
-    while i * (i + 1) // 2 > t:
-        i -= 1
-    return i, t - i * (i + 1) // 2
+def tri_row(t):
+    u = int((math.sqrt(8.0 * t + 1.0) - 1.0) * 0.5)
+    while (u + 1) * (u + 2) // 2 <= t:
+        u += 1
+    while u * (u + 1) // 2 > t:
+        u -= 1
+    return u
 
 
-def aug_factor(A, n, nb, ident):
-    """bo_fit.hip aug_factor on one objective, tile size nb, in place (lower triangle)."""
+def lpart_S(u, base):
+    return u * base + u * (u - 1) // 2
+
+
+def decode(t, k, nbt, ident, TL, nb):
+    """update_role's task decode: (row0, col0, first) of the tile of task t at launch k."""
+    np_ = nbt * nb
+    if t < TL:
+        base = k + 1 if ident else 2
+        bb = 2.0 * base - 1.0
+        u = max(0, int((-bb + math.sqrt(bb * bb + 8.0 * t)) * 0.5))
+        while lpart_S(u + 1, base) <= t:
+            u += 1
+        while lpart_S(u, base) > t:
+            u -= 1
+        c = nbt - 1 - u
+        return (c + (t - lpart_S(u, base))) * nb, c * nb, False
+    t -= TL
+    u = tri_row(t)
+    cp = k - 1 - u
+    b = cp + (t - u * (u + 1) // 2)
+    return np_ + b * nb, np_ + cp * nb, b == k - 1
+
+
+def step_counts(k, nbt, ident):
+    """fit_factor's per-launch counts: panel workgroups, L-part and C-part update tiles."""
+    n_panel = (nbt if ident else nbt - k) if k < nbt else 0
+    TL = TC = 0
+    if k >= 1:
+        m = nbt - 1 - k
+        base = k + 1 if ident else 2
+        TL = m * base + m * (m - 1) // 2 if m > 0 else 0
+        TC = k * (k + 1) // 2 if ident else 0
+    return n_panel, TL, TC
+
+
+def fit_schedule(A, n, nb, ident):
+    """bo_fit.hip fit_factor on one objective (tile nb), in place; returns False on a bad pivot."""
     nbt = -(-n // nb)
-    rb = nbt if ident else 1
-    T = lambda p, q: (slice(p * nb, (p + 1) * nb), slice(q * nb, (q + 1) * nb))  # noqa: E731
+    np_ = nbt * nb
     ok = True
-    for k in range(nbt):
-        ra = min(k + 1, rb) if ident else rb
-        m = nbt - k - 1
-        # chol_panel_kernel: diagonal tile, then the row blocks below (top + live bottom)
-        d = A[T(k, k)]
-        if np.any(~(np.linalg.eigvalsh(np.tril(d) + np.tril(d, -1).T) > 0)):
-            ok = False
-        L = np.linalg.cholesky(np.tril(d) + np.tril(d, -1).T)
-        A[T(k, k)] = L
-        rows = [k + 1 + i for i in range(m)] + [nbt + i for i in range(ra)]
-        for p in rows:
-            A[T(p, k)] = np.linalg.solve(L, A[T(p, k)].T).T           # X L^T = A_pk
-        # chol_update_kernel: T1 top x top, T2 bottom x top, T3 bottom x bottom
-        t1, t2 = m * (m + 1) // 2, ra * m
-        for t in range(t1 + t2 + ra * (ra + 1) // 2):
-            if t < t1:
-                i, j = _tri(t)
-                p, q = k + 1 + i, k + 1 + j
-            elif t < t1 + t2:
-                p, q = nbt + (t - t1) // m, k + 1 + (t - t1) % m
-            else:
-                i, j = _tri(t - t1 - t2)
-                p, q = nbt + i, nbt + j
-            A[T(p, q)] -= A[T(p, k)] @ A[T(q, k)].T
+    steps = nbt + 1 if ident else nbt
+    for k in range(steps):
+        n_panel, TL, TC = step_counts(k, nbt, ident)
+        old = A.copy()                          # every role of launch k reads the launch's input
+        cK, cP = k * nb, (k - 1) * nb
+        for w in range(n_panel):                # panel role: diagonal tile + slab block sb
+            sb = k + 1 + w
+            rows = list(range(cK, cK + nb)) + list(range(sb * nb, sb * nb + nb))
+            C = old[rows, cK:cK + nb].copy()
+            if k > 0:
+                Lr = old[rows, cP:cP + nb].copy()
+                if ident and sb == nbt + k:     # bottom block k: structurally zero in column k-1
+                    Lr[nb:] = 0.0
+                C -= Lr @ old[cK:cK + nb, cP:cP + nb].T
+            D = np.tril(C[:nb])
+            D = D + np.tril(D, -1).T
+            if np.any(~(np.linalg.eigvalsh(D) > 0)):
+                ok = False
+                continue
+            L = np.linalg.cholesky(D)
+            if w == 0:
+                A[cK:cK + nb, cK:cK + nb] = np.tril(L) + np.triu(old[cK:cK + nb, cK:cK + nb], 1)
+            A[sb * nb:sb * nb + nb, cK:cK + nb] = np.linalg.solve(L, C[nb:].T).T
+        tiles = set()
+        for t in range(TL + TC):                # update role: step k-1 on every live tile
+            r0, c0, first = decode(t, k, nbt, ident, TL, nb)
+            assert (r0, c0) not in tiles
+            tiles.add((r0, c0))
+            upd = old[r0:r0 + nb, cP:cP + nb] @ old[c0:c0 + nb, cP:cP + nb].T
+            A[r0:r0 + nb, c0:c0 + nb] = (0.0 if first else old[r0:r0 + nb, c0:c0 + nb]) - upd
+        # the live set the decode enumerates: L part (columns > k, rows from the diagonal to the
+        # live bottom) and, for the inverse, C's lower tiles of the live bottom blocks
+        if k >= 1:
+            rb_hi = nbt + (k if ident else 1)
+            want = {(r * nb, c * nb) for c in range(k + 1, nbt) for r in range(c, rb_hi)}
+            if ident:
+                want |= {(np_ + b * nb, np_ + cp * nb) for cp in range(k) for b in range(cp, k)}
+            assert tiles == want
     return ok
 
 
 def build(km, n, nb, ident, jitter, yc=None):
+    """fit_init_kernel: K + jitter (padding identity), B = I or the one row yc, C unset (NaN:
+    the schedule must never read it before its first contribution)."""
     nbt = -(-n // nb)
-    rb = nbt if ident else 1
-    na = (nbt + rb) * nb
     np_ = nbt * nb
-    A = np.zeros((na, na))
+    na = 2 * np_ if ident else np_ + nb
+    A = np.full((na, na if ident else np_), np.nan)
     A[:np_, :np_] = np.eye(np_)
     A[:n, :n] = km + jitter * np.eye(n)
-    if ident:
+    if ident:                                    # only the tiles b <= j are written (B = I)
+        for b in range(nbt):
+            A[np_ + b * nb:np_ + (b + 1) * nb, b * nb:np_] = 0.0
         A[np_:np_ + n, :n] = np.eye(n)
     else:
+        A[np_:, :] = 0.0
         A[np_, :n] = yc
+    A[np.triu_indices(A.shape[0], 1, A.shape[1])] = np.nan   # never written by the init kernel
     return A, np_
 
 
-@pytest.mark.parametrize("n,nb", [(5, 4), (37, 8), (64, 16), (100, 32)])
+@pytest.mark.parametrize("n,nb", [(5, 4), (37, 8), (64, 16), (100, 32), (70, 8)])
 def test_augmented_inverse_schedule(n, nb):
     rng = np.random.default_rng(n)
     x = rng.uniform(0, 30, size=(n, 2))
     km = np.zeros((1, n, n))
     O.update_k(km, x, 0, n, [3.0], [4.0])
     A, np_ = build(km[0], n, nb, True, 1e-6)
-    assert aug_factor(A, n, nb, True)
+    assert fit_schedule(A, n, nb, True)
     got = -np.tril(A[np_:np_ + n, np_:np_ + n])
     got = got + np.tril(got, -1).T
     ref = O.invert_k(n, km)[0]
     assert np.abs(got - ref).max() <= 1e-9 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("n,nb", [(5, 4), (37, 8), (100, 32)])
+@pytest.mark.parametrize("n,nb", [(5, 4), (37, 8), (100, 32), (70, 8)])
 def test_augmented_mll_schedule(n, nb):
     rng = np.random.default_rng(n + 1)
     x = rng.uniform(0, 30, size=(n, 2))
@@ -92,12 +150,21 @@ def test_augmented_mll_schedule(n, nb):
     km = np.zeros((2, n, n))
     O.update_k(km, x, 0, n, pv, ls)
     tot = 0.0
+    nbt = -(-n // nb)
     for o in range(2):
-        yc = y[:, o] - pm[o]
-        yc = yc / np.std(yc)
+        yc = y[:, o] - pm[o]                    # unscaled: |z|^2 / var(yc) is the data fit
         A, np_ = build(km[o] / pv[o], n, nb, False, 1e-8, yc)
-        assert aug_factor(A, n, nb, False)
-        fit = -A[np_, np_]
+        assert fit_schedule(A, n, nb, False)
+        z = A[np_, :np_]
+        fit = float(np.sum(z * z)) / np.var(yc)
         logdet = 2.0 * np.sum(np.log(np.diag(A)[:n]))
         tot += -0.5 * fit - 0.5 * logdet - 0.5 * n * np.log(2 * np.pi)
+        assert nbt >= 1
     assert tot == pytest.approx(ref, rel=1e-8)   # K/pv here has cond ~1e8: solve-order rounding
+
+
+def test_not_pd_is_flagged():
+    n, nb = 20, 4
+    km = -np.eye(n)
+    A, _ = build(km, n, nb, False, 1e-8, np.zeros(n))
+    assert not fit_schedule(A, n, nb, False)
