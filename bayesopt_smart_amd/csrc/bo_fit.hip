@@ -48,7 +48,32 @@
 namespace {
 
 constexpr int NB = 32;      // column block (panel width) and update tile
+
+// waves per SIMD the step kernel is compiled for (register budget 512 / BO_FIT_WAVES per lane)
+#ifndef BO_FIT_WAVES
+#define BO_FIT_WAVES 2
+#endif
+
+// Diagnostic build (BO_BUILD_VARIANT=DEF_FIT_TIMING): workgroup 0 of every role stamps the
+// 100 MHz real-time clock at its phase boundaries; bo_debug_fit_timing reads them back.
+#ifdef BO_FIT_TIMING
+__device__ long long bo_fit_tstamp[8192];
+__device__ int bo_fit_tcount;
+#define FIT_STAMP(tag)                                                              \
+  do {                                                                              \
+    if ((threadIdx.x & 63) == 0) {                                                  \
+      const int _i = atomicAdd(&bo_fit_tcount, 1);                                  \
+      if (_i < 4096) {                                                              \
+        bo_fit_tstamp[2 * _i] = ((long long)k << 16) | ((long long)blockIdx.x << 4) | (tag); \
+        bo_fit_tstamp[2 * _i + 1] = (long long)wall_clock64();                      \
+      }                                                                             \
+    }                                                                               \
+  } while (0)
+#else
+#define FIT_STAMP(tag) ((void)0)
+#endif
 constexpr int CS = 33;      // LDS row stride (doubles) of the panel tile
+constexpr int FG = 8;       // columns per LDS broadcast group of the panel factorisation
 
 struct FitParams {
   double pv[BO_MAX_OBJ], pm[BO_MAX_OBJ], ls2[BO_MAX_OBJ], jitter;
@@ -66,17 +91,24 @@ struct Geo {
 // partial per step, var(y - pm)); statuses after all objectives' partials
 __host__ __device__ inline int part_len(const Geo& g) { return 2 * g.nbt + 1; }
 
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// 1 / sqrt(x): v_rsq_f64 and two Newton steps (NaN for x <= 0 or NaN: the caller flags the pivot)
-__device__ __forceinline__ double rsqrt_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  double r = __builtin_fma(-x * y, y, 1.0);
-  y = __builtin_fma(0.5 * y, r, y);
-  r = __builtin_fma(-x * y, y, 1.0);
-  return __builtin_fma(0.5 * y, r, y);
+// 1 / sqrt(x) and sqrt(x) from v_rsq_f64 (about 2^-29 relative) by two Goldschmidt steps: g ->
+// sqrt(x), h -> 1 / (2 sqrt(x)); five dependent operations after the rsq.  NaN for x <= 0 or NaN
+// (the caller flags the pivot).
+__device__ __forceinline__ void rsqrt_sqrt(double x, double& rs, double& sq) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  double r = __builtin_fma(-g, h, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  r = __builtin_fma(-g, h, 0.5);
+  sq = __builtin_fma(g, r, g);
+  rs = 2.0 * __builtin_fma(h, r, h);
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -247,7 +279,7 @@ __global__ __launch_bounds__(256) void fit_init_kernel(double* __restrict__ A, G
 
 // ------------------------------------------------------------------------------- step
 // Panel role of launch k, one workgroup per (objective, slab block sb > k); wave 0 factors.
-__device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g, int o, int k, int w_slab,
+__device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g, int o, int k, int w_slab, int n_panel,
                                            double* __restrict__ part, int* __restrict__ status,
                                            double* Cs, double* colb) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -258,6 +290,20 @@ __device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g
   const int lr0 = 16 * wave;                                      // local rows: 0..31 diagonal, 32..63 slab
   const long long grow0 = wave < 2 ? cK + lr0 : (long long)sb * NB + (lr0 - 32);
   const int ntb = wave == 0 ? 1 : 2;                              // rows 0..15: t 16..31 are upper
+  const bool stamp = w_slab == 0 && wave == 0 && o == 0;
+  const bool stamp_last = w_slab == n_panel - 1 && wave == 0 && o == g.n_obj - 1;
+  if (stamp) FIT_STAMP(1);
+  if (stamp_last) FIT_STAMP(5);
+  // this wave's A values at its D positions (t = 16 tb + lg + 4 i, row grow0 + li), issued first
+  // with the operand loads: one memory round trip before the MFMAs
+  double av_a[2][4];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 16 * tb + lg + 4 * i;
+      av_a[tb][i] = (tb < ntb && !(wave < 2 && lr0 + li < t)) ? Ao[(cK + t) * Na + grow0 + li] : 0.0;
+    }
   d4 acc[2];
   acc[0] = (d4){0.0, 0.0, 0.0, 0.0};
   acc[1] = acc[0];
@@ -287,45 +333,71 @@ __device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g
     for (int i = 0; i < 4; ++i) {
       const int t = 16 * tb + lg + 4 * i;
       const int rl = lr0 + li;
-      double v = 0.0;
-      if (tb < ntb && !(wave < 2 && rl < t)) v = Ao[(cK + t) * Na + grow0 + li] - acc[tb][i];
-      Cs[rl * CS + t] = v;
+      Cs[rl * CS + t] = av_a[tb][i] - acc[tb][i];               // masked entries: 0 - 0
     }
+  if (stamp) FIT_STAMP(2);
   __syncthreads();
+  if (stamp_last) FIT_STAMP(6);
   if (wave != 0) return;
   double a[NB];
 #pragma unroll
   for (int t = 0; t < NB; ++t) a[t] = Cs[lane * CS + t];
+  const long long row_l = lane < NB ? cK + lane : (long long)sb * NB + lane - NB;   // this lane's row
+  // column block k as a buffer resource: element (row, cK + j) at row * 8 + j * col_bytes
+  const int col_bytes = (int)(Na * 8);
+  const __amdgpu_buffer_rsrc_t colr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Ao + cK * Na), (short)0, NB * col_bytes, 0x00020000);
+  const int row_off = (int)(row_l * 8);
   double dj = 1.0;
   bool bad = false;
+  // Groups of FG columns: inside a group each new column reaches the group's later columns by
+  // v_readlane (the pivot chain: readlane -> rsqrt -> mul -> readlane -> fma); at the end of the
+  // group its FG columns reach the remaining columns through ONE LDS round trip (lanes 0..31 store
+  // their FG values, every lane reads row t's FG values as a broadcast) -- 4 LDS round trips on
+  // the chain instead of 32 (one per column: 4.5 us per factorisation measured).
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const double piv = bo_readlane_d(a[j], j);
-    bad = bad || !(piv > 0.0);                                   // potrf: a_jj <= 0 or NaN
-    const double rs = rsqrt_nr(piv);
-    const double d = piv * rs;
-    a[j] = lane == j ? d : a[j] * rs;                           // lanes > j: L_ij; lanes < j: unused
-    dj = lane == j ? d : dj;
-    if (j + 1 < NB) {
-      const double l1 = bo_readlane_d(a[j], j + 1);             // L(j+1, j): the next pivot first
-      a[j + 1] = __builtin_fma(-a[j], l1, a[j + 1]);
-      if (j + 2 < NB) {
-        if (lane < NB) colb[j * NB + lane] = a[j];
-        wave_lds_sync();
+  for (int j0 = 0; j0 < NB; j0 += FG) {
 #pragma unroll
-        for (int t = j + 2; t < NB; ++t) a[t] = __builtin_fma(-a[j], colb[j * NB + t], a[t]);
+    for (int j = j0; j < j0 + FG; ++j) {
+      const double piv = bo_readlane_d(a[j], j);
+      bad = bad || !(piv > 0.0);                                 // potrf: a_jj <= 0 or NaN
+      double rs, d;
+      rsqrt_sqrt(piv, rs, d);
+      a[j] = lane == j ? d : a[j] * rs;                         // lanes > j: L_ij; lanes < j: unused
+      dj = lane == j ? d : dj;
+      // column j is final: store it now (diagonal rows >= j by workgroup 0, every slab row), so
+      // that the stores drain under the rest of the factorisation
+      // (a buffer store: the lane's row offset in one VGPR, the column offset in an SGPR -- plain
+      // stores kept 32 64-bit addresses live and spilled)
+      // branch-free: the lanes that must not store get an offset past the resource (dropped)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, a[j]), colr,
+                                            (lane >= NB || (w_slab == 0 && lane >= j)) ? row_off : 0x40000000,
+                                            j * col_bytes, 0);
+#pragma unroll
+      for (int t = j + 1; t < j0 + FG; ++t) a[t] = __builtin_fma(-a[j], bo_readlane_d(a[j], t), a[t]);
+    }
+    if (j0 + FG < NB) {
+      if (lane < NB) {
+#pragma unroll
+        for (int c = 0; c < FG; ++c) colb[lane * FG + c] = a[j0 + c];
       }
+      wave_lds_sync();
+#pragma unroll
+      for (int t = j0 + FG; t < NB; ++t) {
+        double s0 = a[t];
+#pragma unroll
+        for (int c = 0; c < FG; ++c) s0 = __builtin_fma(-a[j0 + c], colb[t * FG + c], s0);
+        a[t] = s0;
+      }
+      wave_lds_sync();                                           // colb is rewritten by the next group
     }
   }
-  // L_kk (one workgroup writes it) and the slab's L rows
-  if (w_slab == 0) {
-#pragma unroll
-    for (int t = 0; t < NB; ++t)
-      if (lane < NB && t <= lane) Ao[(cK + t) * Na + cK + lane] = a[t];
-  }
-#pragma unroll
-  for (int t = 0; t < NB; ++t)
-    if (lane >= NB) Ao[(cK + t) * Na + (long long)sb * NB + lane - NB] = a[t];
+  if (stamp) FIT_STAMP(3);
+#ifdef BO_FIT_TIMING
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (stamp) FIT_STAMP(4);
+  if (stamp_last) FIT_STAMP(7);
+#endif
   if (g.ident) {
     if (w_slab == 0 && bad && lane == 0) atomicOr(status + o, 1);
     return;
@@ -384,6 +456,19 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
   double* Ao = A + (long long)o * g.ostride;
   const long long Na = g.Na;
   const double* Lp = Ao + (long long)(k - 1) * NB * Na;
+  const bool stamp = wt == 0;
+  const bool stamp_last = wt == per * g.n_obj - 1;
+  if (stamp) FIT_STAMP(8);
+  if (stamp_last) FIT_STAMP(10);
+  // the tile's current values first (one memory round trip with the operands)
+  double cv[2][2][4];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        cv[tb][rb][i] = first ? 0.0 : Ao[(col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li];
   double av[2][8], bv[2][8];
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks)
@@ -409,14 +494,17 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        double* c = Ao + (col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li;
-        *c = (first ? 0.0 : *c) - acc[tb][rb][i];
-      }
+      for (int i = 0; i < 4; ++i)
+        Ao[(col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li] = cv[tb][rb][i] - acc[tb][rb][i];
+#ifdef BO_FIT_TIMING
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (stamp) FIT_STAMP(9);
+  if (stamp_last) FIT_STAMP(11);
+#endif
 }
 
 // Launch k: blocks [0, n_obj * n_panel) panel role, the rest update role (4 tiles per block).
-__global__ __launch_bounds__(256) void fit_step_kernel(double* __restrict__ A, Geo g, int k, int n_panel,
+__global__ __launch_bounds__(256, BO_FIT_WAVES) void fit_step_kernel(double* __restrict__ A, Geo g, int k, int n_panel,
                                                        long long TL, long long TC,
                                                        double* __restrict__ part, int* __restrict__ status) {
   __shared__ double Cs[2 * NB * CS];
@@ -424,7 +512,7 @@ __global__ __launch_bounds__(256) void fit_step_kernel(double* __restrict__ A, G
   const int np = g.n_obj * n_panel;
   if ((int)blockIdx.x < np) {
     const int o = blockIdx.x / n_panel;
-    panel_role(A + (long long)o * g.ostride, g, o, k, blockIdx.x % n_panel, part, status, Cs, colb);
+    panel_role(A + (long long)o * g.ostride, g, o, k, blockIdx.x % n_panel, n_panel, part, status, Cs, colb);
   } else {
     update_role(A, g, k, TL, TC, ((long long)blockIdx.x - np) * 4 + (threadIdx.x >> 6));
   }
@@ -698,6 +786,23 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
   }
   return BO_OK;
 }
+
+#ifdef BO_FIT_TIMING
+// diagnostic build only: the phase stamps of the step launches since the last call (pairs of
+// (k << 16 | block << 4 | tag, 100 MHz clock)); returns the count and resets it
+int bo_debug_fit_timing(long long* out, int cap) {
+  int cnt = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(bo_fit_tcount), sizeof(int)) != hipSuccess) return -1;
+  if (cnt > 4096) cnt = 4096;
+  if (cnt > cap) cnt = cap;
+  if (cnt > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_fit_tstamp), sizeof(long long) * 2 * cnt) != hipSuccess)
+    return -1;
+  const int zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(bo_fit_tcount), &zero, sizeof(int)) != hipSuccess) return -1;
+  return cnt;
+}
+#endif
 
 size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n) {
   if (n_obj < 1 || n < 1) return 0;
