@@ -147,11 +147,13 @@ def hypervolume_improvement_exact(ucb, front, reference_point, prior_mean, prior
 
 
 def hvi_select_indices(acquisition_values, ucb, y_vector, n_evaluations, reference_point, prior_mean,
-                       prior_variance, cands, evaluated_points, batch_size):
+                       prior_variance, cands, evaluated_points, batch_size, offset=0, return_record=False):
     """The exact-HVI acquisition AND its batch selection in one device pass (bo_hvi_select_topq,
-    batch_size <= BO_MAX_TOPQ): acquisition_values (device, [M]) receives the HVI of every candidate's
-    UCB vector over the Pareto front of y_vector[:n_evaluations]; returns the global indices of
-    the best batch_size candidates not equal to an evaluated point (select_next_batch's order)."""
+    batch_size <= BO_MAX_TOPQ): acquisition_values (device, [count]) receives the HVI of the UCB
+    vector of every candidate of the shard [offset, offset + count) over the Pareto front of
+    y_vector[:n_evaluations]; returns the global indices of the shard's best batch_size candidates
+    not equal to an evaluated point (select_next_batch's order) -- or, `return_record`, the device
+    record block [2 batch_size] (values, bit-cast int64 indices) for the multi-rank exchange."""
     from .pareto import is_pareto_efficient
     if batch_size > _lib.MAX_TOPQ:
         raise ValueError(f"hvi_select_indices handles batch_size <= {_lib.MAX_TOPQ}")
@@ -174,13 +176,18 @@ def hvi_select_indices(acquisition_values, ucb, y_vector, n_evaluations, referen
     sh = (C_i64 * 8)(*(list(cands.shape or []) + [1] * (8 - len(cands.shape or []))))
     shift = _host_vec(prior_mean, n_obj)
     scale = _host_vec(np.sqrt(np.asarray(prior_variance, dtype=np.float64)), n_obj)
+    carg = cands.cand_arg
+    if cands.kind in ("i64", "f64"):            # explicit candidates: the shard's rows
+        carg = cands.tensor[offset:].data_ptr()
     _lib.check(lib.bo_hvi_select_topq(acq.ptr, u.ptr, u.t.stride(0), n, n_obj, shift, scale,
                                       boxes.data_ptr() if boxes.numel() else None, boxes.shape[0],
-                                      cands.kind_code, cands.cand_arg, lo, sh, cands.dim, 0,
+                                      cands.kind_code, carg, lo, sh, cands.dim, offset,
                                       ex.data_ptr() if ex.numel() else None, ex.shape[0], batch_size,
                                       rec.data_ptr(), rec.data_ptr() + 8 * batch_size, ws.data_ptr(),
                                       ws.numel(), stream_handle(dev)), "bo_hvi_select_topq")
     acq.finish()
+    if return_record:
+        return rec
     idx = rec[batch_size:].view(torch.int64).cpu().numpy()
     return idx[idx >= 0]
 

@@ -10,6 +10,12 @@ inner loop (bayesian_optimization.py:108-247) on the MI355X:
                      buffer of the reference is never allocated
   evaluation         the user's objective on the host (unchanged)
 
+Multi-GPU (one process per GPU, torch.distributed over RCCL): every rank runs the loop; the
+candidate set is sharded over the ranks (distributed.shard_range), each rank scores its shard
+and ONE all_gather of the per-rank top-q records selects the batch.  The fit is replicated
+(rank 0's hyper-parameters are broadcast), the objective is evaluated on rank 0 and its values
+broadcast.
+
 Posterior arrays stay in HBM; callbacks receive a ``state`` dict whose array entries are
 copied to numpy only when a callback reads them.
 """
@@ -54,8 +60,9 @@ class LazyState(dict):
 
 
 class DeviceBuffers:
-    """The reference's preallocated posterior arrays (bayesian_optimization.py:355-401), in HBM.
-    k_star (n_obj x T x M) is not among them: the fused kernel never materialises it."""
+    """The reference's preallocated posterior arrays (bayesian_optimization.py:355-401), in HBM,
+    over `m` candidates (this rank's shard).  k_star (n_obj x T x M) is not among them: the fused
+    kernel never materialises it."""
 
     def __init__(self, n_obj, total, m, dev):
         z = lambda *s: torch.zeros(s, dtype=F64, device=dev)  # noqa: E731
@@ -68,40 +75,122 @@ class DeviceBuffers:
         self.acquisition_values = z(m)
 
 
-def _predict_select(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
-                    buffers: DeviceBuffers, batch_size, evaluated, acquisition="sum_ucb",
-                    y_evaluated=None, reference_point=None):
-    """The fused predict + acquisition + select step; returns x_next (int64 rows).
+def _world(group=None):
+    """(rank, world size) of the torch.distributed group; (0, 1) when not initialised."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
 
-    acquisition "sum_ucb" is the reference's (acquisition.py:89-108, fused top-q);
-    "hvi" replaces the acquisition array with the exact hypervolume improvement of the UCB
-    vectors over the Pareto front of `y_evaluated` above `reference_point` (device scan), then
-    selects with the standalone device top-q."""
-    out = {"mu": buffers.mu_objectives, "var": buffers.variance_objectives,
-           "std_mu": buffers.std_mu_objectives, "std_var": buffers.std_variance_objectives,
-           "ucb": buffers.ucb, "acq": buffers.acquisition_values}
-    q = batch_size if batch_size <= _lib.MAX_TOPQ and acquisition == "sum_ucb" else 0
-    r = predict_acquire(x_dev, y_dev, kinv, cands, prior_mean, prior_variance, length_scales, betas,
-                        outputs=tuple(out), topq=q, out=out)
-    if acquisition == "hvi" and batch_size <= _lib.MAX_TOPQ:
-        # exact HVI and its top-q with exclusion in one device pass
-        idx = hvi_select_indices(buffers.acquisition_values, buffers.ucb, y_evaluated, len(y_evaluated),
-                                 reference_point, prior_mean, prior_variance, cands, evaluated, batch_size)
-        return cands.points(idx) if idx.size else np.zeros((0, cands.dim), dtype=np.int64)
-    if acquisition == "hvi":
-        update_hypervolume_improvement_exact(buffers.acquisition_values, buffers.ucb, y_evaluated,
-                                             len(y_evaluated), reference_point, prior_mean,
-                                             prior_variance)
-    elif acquisition != "sum_ucb":
-        raise ValueError(f"unknown acquisition {acquisition!r} (expected 'sum_ucb' or 'hvi')")
-    if q:
-        idx = r["top_idx"].cpu().numpy()
-        idx = idx[idx >= 0]
-    else:  # batches above BO_MAX_TOPQ: rounds of the standalone device selection
-        idx = select_indices(buffers.acquisition_values, cands, evaluated, batch_size)
-    if idx.size == 0:
-        return np.zeros((0, cands.dim), dtype=np.int64)
-    return cands.points(idx)
+
+def _broadcast_np(arr, group=None):
+    """Broadcast a float64 numpy array (or view) from rank 0 in place; a no-op on one rank.  The
+    collective's tensor lives where the backend needs it (HIP for RCCL, host for gloo)."""
+    import torch.distributed as dist
+    _, world = _world(group)
+    if world == 1 or np.size(arr) == 0:
+        return arr
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+        else torch.device("cpu")
+    t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float64), device=dev)
+    dist.broadcast(t, 0, group=group)
+    arr[...] = t.cpu().numpy().reshape(np.shape(arr))
+    return arr
+
+
+class DeviceBackend:
+    """The device side of one loop iteration (bayesian_optimization.py:115-207) on this rank:
+
+      fit      Powell on the device MLL (every evaluation one bo_compute_mll call), rank 0's
+               hyper-parameters broadcast, then update_k + invert_k (bo_update_k, bo_invert_k);
+      select   the fused predict + acquisition + top-q (bo_predict_acquire) over this rank's
+               candidate shard -- the whole set on one rank; shard_range(M, rank, P) and ONE
+               all_gather of the 16-B top-q records with P ranks (sharded_predict_acquire) --
+               returning the global batch's candidate indices, identical on every rank.
+
+    `state_arrays` gives the callbacks' mu / variance / acquisition arrays over the whole set:
+    this rank's buffers, or the shards gathered (a collective: every rank's loop calls it at the
+    same point)."""
+
+    def __init__(self, cands, n_obj, total_samples, device=None, buffers=None, group=None):
+        from .distributed import shard_range
+        self.dev = require_device(device)
+        self.cands = cands
+        self.group = group
+        self.rank, self.world = _world(group)
+        self.offset, self.count = shard_range(cands.n, self.rank, self.world)
+        if buffers is None:
+            buffers = DeviceBuffers(n_obj, total_samples, self.count, self.dev)
+        self.bufs = buffers
+
+    def fit(self, x_vector, y_vector, n, prior_mean, prior_variance, length_scales):
+        """Returns (Powell's OptimizeResult, fitted device state, time after the Powell fit)."""
+        xd = torch.as_tensor(np.ascontiguousarray(x_vector[:n], dtype=np.float64), device=self.dev)
+        yd = torch.as_tensor(np.ascontiguousarray(y_vector[:n], dtype=np.float64), device=self.dev)
+        optimized = K.optimize_hyperparams_mll(xd, yd, self.bufs.kernel_matrices, prior_mean,
+                                               prior_variance, length_scales, n)
+        _broadcast_np(length_scales, self.group)
+        _broadcast_np(prior_variance, self.group)
+        t1 = time.perf_counter()
+        K.update_k(self.bufs.kernel_matrices, xd, 0, n, prior_variance, length_scales)
+        kinv = K.invert_k(n, self.bufs.kernel_matrices)
+        torch.cuda.synchronize(self.dev)
+        return optimized, (xd, yd, kinv), t1
+
+    def _outputs(self):
+        b = self.bufs
+        return {"mu": b.mu_objectives, "var": b.variance_objectives, "std_mu": b.std_mu_objectives,
+                "std_var": b.std_variance_objectives, "ucb": b.ucb, "acq": b.acquisition_values}
+
+    def select(self, fitted, prior_mean, prior_variance, length_scales, betas, batch_size, evaluated,
+               acquisition="sum_ucb", y_evaluated=None, reference_point=None):
+        """Global candidate indices of the next batch (select_next_batch's order, the evaluated
+        points excluded).  "sum_ucb" is the reference's acquisition (acquisition.py:89-108, fused
+        top-q); "hvi" replaces the acquisition array with the exact hypervolume improvement of the
+        UCB vectors over the Pareto front of `y_evaluated` above `reference_point`."""
+        if acquisition not in ("sum_ucb", "hvi"):
+            raise ValueError(f"unknown acquisition {acquisition!r} (expected 'sum_ucb' or 'hvi')")
+        xd, yd, kinv = fitted
+        out = self._outputs()
+        if acquisition == "sum_ucb" and batch_size <= _lib.MAX_TOPQ:
+            from .distributed import sharded_predict_acquire
+            _, (_, idx) = sharded_predict_acquire(xd, yd, kinv, self.cands, prior_mean, prior_variance,
+                                                  length_scales, betas, batch_size, outputs=tuple(out),
+                                                  group=self.group, device=self.dev, out=out)
+            return np.asarray(idx, dtype=np.int64)
+        predict_acquire(xd, yd, kinv, self.cands, prior_mean, prior_variance, length_scales, betas,
+                        outputs=tuple(out), topq=0, offset=self.offset, count=self.count, out=out,
+                        device=self.dev)
+        if acquisition == "hvi" and batch_size <= _lib.MAX_TOPQ:
+            # the exact HVI and its top-q with exclusion in one device pass over this shard, then
+            # the fused path's exchange
+            rec = hvi_select_indices(self.bufs.acquisition_values, self.bufs.ucb, y_evaluated,
+                                     len(y_evaluated), reference_point, prior_mean, prior_variance,
+                                     self.cands, evaluated, batch_size, offset=self.offset,
+                                     return_record=True)
+            if self.world == 1:
+                idx = rec[batch_size:].view(torch.int64).cpu().numpy()
+                return idx[idx >= 0]
+            from .distributed import exchange_topq_rec
+            return np.asarray(exchange_topq_rec(rec, batch_size, self.group)[1], dtype=np.int64)
+        if acquisition == "hvi":
+            update_hypervolume_improvement_exact(self.bufs.acquisition_values, self.bufs.ucb, y_evaluated,
+                                                 len(y_evaluated), reference_point, prior_mean,
+                                                 prior_variance)
+        # batches above BO_MAX_TOPQ: rounds of the standalone device selection (over the gathered
+        # array when sharded)
+        acq = self.bufs.acquisition_values if self.world == 1 else \
+            torch.as_tensor(self.state_arrays()["acquisition_values"], device=self.dev)
+        return select_indices(acq, self.cands, evaluated, batch_size)
+
+    def state_arrays(self):
+        b = self.bufs
+        arrs = {"mu_objectives": b.mu_objectives, "variance_objectives": b.variance_objectives,
+                "acquisition_values": b.acquisition_values}
+        if self.world == 1:
+            return arrs
+        from .distributed import gather_shards
+        return {k: gather_shards(v, self.cands.n, self.group) for k, v in arrs.items()}
 
 
 def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, variance_objectives,
@@ -109,7 +198,7 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
              prior_mean, prior_variance, reference_point, n_evaluations, total_samples,
              n_objectives, function, betas, length_scales, batch_size, bounds,
              callbacks: Optional[List[Callable]] = None, *,
-             acquisition: str = "sum_ucb") -> Tuple[np.ndarray, np.ndarray, int]:
+             acquisition: str = "sum_ucb", group=None, backend=None) -> Tuple[np.ndarray, np.ndarray, int]:
     """bayesian_optimization.py:51-247 with the reference's argument list.
 
     `kernel_matrices` and the posterior arrays may be HIP tensors (in place) or numpy arrays;
@@ -117,59 +206,68 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
     materialised); `input_space` may be a CandidateSet, a device tensor or the reference's
     int64 numpy array.  Returns (x_vector, y_vector, last_eval + 1) like the reference
     (including its count quirk, :247).
+
+    With torch.distributed initialised (one process per GPU) every rank runs this loop over its
+    shard of the candidates (module docstring); the posterior arrays given here are then not
+    filled (each rank holds its shard), the state dict's arrays are the gathered whole.  `group`
+    selects the process group; `backend` replaces the device side (DeviceBackend's interface:
+    fit / select / state_arrays / cands / rank / world / bufs).
     """
-    dev = require_device()
     del k_star, n_objectives, bounds  # unused, as in the reference (reference_point too, unless
     #                                   acquisition="hvi", the exact hypervolume improvement)
-    cands = input_space if isinstance(input_space, CandidateSet) else CandidateSet.explicit(input_space, dev)
     n_obj = len(prior_mean)
+    if backend is None:
+        dev = require_device()
+        cands = input_space if isinstance(input_space, CandidateSet) else CandidateSet.explicit(input_space, dev)
+        from .distributed import shard_range
+        _, world = _world(group)
+        cnt = shard_range(cands.n, _world(group)[0], world)[1]
 
-    def dev_buf(a, shape):
-        if isinstance(a, torch.Tensor) and a.device.type == "cuda":
-            return a
-        return torch.zeros(shape, dtype=F64, device=dev)
+        def dev_buf(a, shape):
+            if isinstance(a, torch.Tensor) and a.device.type == "cuda" and tuple(a.shape) == shape:
+                return a
+            return torch.zeros(shape, dtype=F64, device=dev)
 
-    m = cands.n
-    bufs = DeviceBuffers.__new__(DeviceBuffers)
-    bufs.kernel_matrices = dev_buf(kernel_matrices, (n_obj, total_samples, total_samples))
-    bufs.mu_objectives = dev_buf(mu_objectives, (n_obj, m))
-    bufs.variance_objectives = dev_buf(variance_objectives, (n_obj, m))
-    bufs.std_mu_objectives = dev_buf(std_mu_objectives, (n_obj, m))
-    bufs.std_variance_objectives = dev_buf(std_variance_objectives, (n_obj, m))
-    bufs.ucb = dev_buf(ucb, (n_obj, m))
-    bufs.acquisition_values = dev_buf(acquisition_values, (m,))
+        bufs = DeviceBuffers.__new__(DeviceBuffers)
+        bufs.kernel_matrices = dev_buf(kernel_matrices, (n_obj, total_samples, total_samples))
+        bufs.mu_objectives = dev_buf(mu_objectives, (n_obj, cnt))
+        bufs.variance_objectives = dev_buf(variance_objectives, (n_obj, cnt))
+        bufs.std_mu_objectives = dev_buf(std_mu_objectives, (n_obj, cnt))
+        bufs.std_variance_objectives = dev_buf(std_variance_objectives, (n_obj, cnt))
+        bufs.ucb = dev_buf(ucb, (n_obj, cnt))
+        bufs.acquisition_values = dev_buf(acquisition_values, (cnt,))
+        backend = DeviceBackend(cands, n_obj, total_samples, dev, bufs, group)
+    cands, rank, world = backend.cands, backend.rank, backend.world
 
     last_eval = 0
     for current_eval in range(n_evaluations, total_samples, batch_size):
         iter_start = time.perf_counter()
         t0 = time.perf_counter()
-        xd = torch.as_tensor(np.ascontiguousarray(x_vector[:current_eval], dtype=np.float64), device=dev)
-        yd = torch.as_tensor(np.ascontiguousarray(y_vector[:current_eval], dtype=np.float64), device=dev)
-        optimized = K.optimize_hyperparams_mll(xd, yd, bufs.kernel_matrices, prior_mean, prior_variance,
-                                               length_scales, current_eval)
-        t1 = time.perf_counter()
-        K.update_k(bufs.kernel_matrices, xd, 0, current_eval, prior_variance, length_scales)
-        kinv = K.invert_k(current_eval, bufs.kernel_matrices)
-        torch.cuda.synchronize(dev)
+        optimized, fitted, t1 = backend.fit(x_vector, y_vector, current_eval, prior_mean, prior_variance,
+                                            length_scales)
         t2 = time.perf_counter()
-        x_next = _predict_select(xd, yd, kinv, cands, prior_mean, prior_variance, length_scales, betas,
-                                 bufs, batch_size, x_vector[:current_eval], acquisition,
-                                 y_vector[:current_eval], reference_point)
+        idx = backend.select(fitted, prior_mean, prior_variance, length_scales, betas, batch_size,
+                             x_vector[:current_eval], acquisition, y_vector[:current_eval], reference_point)
+        x_next = cands.points(idx) if idx.size else np.zeros((0, cands.dim), dtype=np.int64)
         t3 = time.perf_counter()
         for b_idx, point in enumerate(x_next):
             x_vector[current_eval + b_idx] = point
-            y_vector[current_eval + b_idx] = function(point)
+            if rank == 0:       # the user's objective, once per point (bayesian_optimization.py:213-216)
+                y_vector[current_eval + b_idx] = function(point)
+        if world > 1:
+            _broadcast_np(y_vector[current_eval:current_eval + len(x_next)], backend.group)
         last_eval = current_eval
         t4 = time.perf_counter()
         if callbacks:
+            arrs = backend.state_arrays()
             state = LazyState({
                 "iteration": current_eval,
                 "n_evaluations": current_eval + batch_size,
                 "x_vector": x_vector[: current_eval + batch_size],
                 "y_vector": y_vector[: current_eval + batch_size],
-                "mu_objectives": bufs.mu_objectives,
-                "variance_objectives": bufs.variance_objectives,
-                "acquisition_values": bufs.acquisition_values,
+                "mu_objectives": arrs["mu_objectives"],
+                "variance_objectives": arrs["variance_objectives"],
+                "acquisition_values": arrs["acquisition_values"],
                 "x_next": x_next,
                 "hyperparams": optimized.x,
                 "timings": {"hyperparams": t1 - t0, "kernels": t2 - t1, "acquisition": t3 - t2,
@@ -177,15 +275,17 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
             })
             for cb in callbacks:
                 cb(state)
-    if isinstance(kernel_matrices, np.ndarray):   # the reference mutates it in place (update_k)
-        kernel_matrices[...] = bufs.kernel_matrices.cpu().numpy().reshape(kernel_matrices.shape)
-    for name, a in (("mu", mu_objectives), ("var", variance_objectives), ("smu", std_mu_objectives),
-                    ("svar", std_variance_objectives), ("ucb", ucb), ("acq", acquisition_values)):
-        if isinstance(a, np.ndarray):   # numpy callers get their arrays filled, as in the reference
-            src = {"mu": bufs.mu_objectives, "var": bufs.variance_objectives,
-                   "smu": bufs.std_mu_objectives, "svar": bufs.std_variance_objectives,
-                   "ucb": bufs.ucb, "acq": bufs.acquisition_values}[name]
-            a[...] = src.cpu().numpy()
+    bufs = getattr(backend, "bufs", None)
+    if bufs is not None and world == 1:
+        if isinstance(kernel_matrices, np.ndarray):   # the reference mutates it in place (update_k)
+            kernel_matrices[...] = bufs.kernel_matrices.cpu().numpy().reshape(kernel_matrices.shape)
+        for name, a in (("mu", mu_objectives), ("var", variance_objectives), ("smu", std_mu_objectives),
+                        ("svar", std_variance_objectives), ("ucb", ucb), ("acq", acquisition_values)):
+            if isinstance(a, np.ndarray):   # numpy callers get their arrays filled, as in the reference
+                src = {"mu": bufs.mu_objectives, "var": bufs.variance_objectives,
+                       "smu": bufs.std_mu_objectives, "svar": bufs.std_variance_objectives,
+                       "ucb": bufs.ucb, "acq": bufs.acquisition_values}[name]
+                a[...] = src.cpu().numpy()
     return x_vector, y_vector, last_eval + 1
 
 
@@ -217,13 +317,17 @@ class BayesianOptimization:
     Extra kwargs (not in the reference): ``input_space`` (explicit [M, d] candidates, e.g.
     a Sobol set, instead of the integer grid), ``device``, ``acquisition`` ("sum_ucb", the
     reference's default, or "hvi": exact hypervolume improvement of the UCB vectors over the
-    evaluated Pareto front) and ``reference_point`` (the HVI reference point; the reference
-    fixes it at zeros and never uses it, bayesian_optimization.py:425).
+    evaluated Pareto front), ``reference_point`` (the HVI reference point; the reference
+    fixes it at zeros and never uses it, bayesian_optimization.py:425) and ``group`` (the
+    torch.distributed process group of a multi-GPU run; default: the world when initialised).
+    With several ranks, each holds its shard of the posterior arrays, the initial design's
+    objective values are rank 0's (broadcast) and the loop runs as `optimize` describes.
     """
 
     def __init__(self, function: Callable[[np.ndarray], np.ndarray], bounds: List[Tuple[int, int]],
                  n_objectives: int = 3, n_iterations: int = 10, **kwargs: Any):
         self.device = require_device(kwargs.get("device"))
+        self.group = kwargs.get("group")
         self.function = function
         self.bounds = bounds
         self.n_objectives = n_objectives
@@ -251,11 +355,16 @@ class BayesianOptimization:
         _check_limits(n_objectives, self.dim, self.total_samples, self.batch_size, self.acquisition)
         self.x_vector = np.zeros((self.total_samples, self.dim), dtype=NUMBA_FLOAT_TYPE)
         self.y_vector = np.zeros((self.total_samples, n_objectives), dtype=NUMBA_FLOAT_TYPE)
-        self._buffers = DeviceBuffers(n_objectives, self.total_samples, self.candidates.n, self.device)
+        self._backend = DeviceBackend(self.candidates, n_objectives, self.total_samples, self.device,
+                                      group=self.group)
+        self._buffers = self._backend.bufs
         self.k_star = None   # never materialised (the reference allocates n_obj x T x M here)
         self.n_evaluations = K.initialize_lhs_integer(self.x_vector, self.y_vector,
                                                       np.array(self.bounds, dtype=np.int64),
                                                       self.function, self.initial_samples)
+        # several ranks: rank 0's initial design is everyone's
+        _broadcast_np(self.x_vector[: self.n_evaluations], self.group)
+        _broadcast_np(self.y_vector[: self.n_evaluations], self.group)
         if np.all(self.prior_mean == DEFAULT_PRIOR_MEAN):
             self.prior_mean = K.compute_prior_mean(self.y_vector, self.n_evaluations, n_objectives)
         if np.all(self.prior_variance == DEFAULT_PRIOR_VARIANCE):
@@ -294,7 +403,7 @@ class BayesianOptimization:
             total_samples=self.total_samples, n_objectives=self.n_objectives, function=self.function,
             betas=self.betas, length_scales=self.length_scales, batch_size=self.batch_size,
             bounds=self.bounds, callbacks=self.callbacks if self.callbacks else None,
-            acquisition=self.acquisition)
+            acquisition=self.acquisition, group=self.group, backend=self._backend)
 
     def pareto_analysis(self) -> np.ndarray:
         """bayesian_optimization.py:465-488."""

@@ -88,12 +88,33 @@ def front_hypervolume(front, reference_point, group=None, device=None, partial=N
     return float(np.prod(upper - r) - val.item())
 
 
+def gather_shards(t, n, group=None):
+    """The whole array from every rank's contiguous shard (shard_range(n, r, P) along the last
+    axis): ONE all_gather of the shards padded to the largest, then trimmed.  A collective; on the
+    backend's device (HIP for RCCL, host for gloo).  Returns a tensor [..., n]."""
+    world = dist.get_world_size(group)
+    dev = t.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    counts = [shard_range(n, r, world)[1] for r in range(world)]
+    cmax = max(counts)
+    lead = tuple(t.shape[:-1])
+    pad = torch.zeros(lead + (cmax,), dtype=t.dtype, device=dev)
+    pad[..., :t.shape[-1]] = t.to(dev)
+    g = torch.empty(world * pad.numel(), dtype=t.dtype, device=dev)
+    dist.all_gather_into_tensor(g, pad.reshape(-1), group=group)
+    g = g.view((world,) + lead + (cmax,))
+    return torch.cat([g[r, ..., :counts[r]] for r in range(world)], dim=-1)
+
+
 def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
-                            betas, q, outputs=("acq",), group=None, device=None, scorer=None):
+                            betas, q, outputs=("acq",), group=None, device=None, scorer=None, out=None,
+                            mode="auto"):
     """Score this rank's shard of `cands` and return (local results, global top-q).
 
-    `scorer` replaces predict_acquire with the same keyword interface (tests drive the
-    partition and the exchange on CPU ranks with the oracle standing in for the device)."""
+    Rank r scores candidates shard_range(M, r, P) (its outputs, [n_obj, count] / [count], go to
+    `out` when given); the global top-q (NaN first, descending value, ascending index, evaluated
+    points excluded) comes from ONE all_gather of the ranks' 16-B record blocks.  `scorer`
+    replaces predict_acquire with the same keyword interface (tests drive the partition and the
+    exchange on CPU ranks with the oracle standing in for the device)."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     off, cnt = shard_range(cands.n, rank, world)
@@ -107,6 +128,10 @@ def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_var
         kw = {}
     if q > 0:
         kw["top_rec"] = torch.empty(2 * q, dtype=torch.float64, device=dev)
+    if out is not None:
+        kw["out"] = out
+    if scorer is None:
+        kw["mode"] = mode
     r = score(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales, betas,
               outputs=outputs, topq=q, offset=off, count=cnt, **kw)
     if world == 1:

@@ -7,9 +7,11 @@
 Workload (BASELINE.json configs[2], "C3"): 2-D / 2-objective toy_function
 (examples/benchmark_functions.py:33-50), N_train = 512, 1,048,576 candidates per GPU on the
 reference's integer 'ij' grid (bayesian_optimization.py:338-340), length scales 20, betas 2,
-q = 3 (select_next_batch with the evaluated points excluded).  Weak scaling: rank r scores
-rows [1024 r, 1024 (r + 1)) of a (1024 N) x 1024 grid; the per-rank top-q lists meet in one
-RCCL all_gather, merged on rank 0.
+q = 3 (select_next_batch with the evaluated points excluded).  Strong scaling (the default): the
+fixed 1,048,576-candidate grid of BASELINE's config is split into P contiguous index ranges
+(distributed.shard_range), the training set independent of P; the per-rank top-q lists meet in
+one RCCL all_gather.  --scaling weak: rank r scores rows [1024 r, 1024 (r + 1)) of a
+(1024 P) x 1024 grid instead.
 
 One step = one bo_predict_acquire call per rank (K^-1 packing, alpha = K^-1 (y - pm), the
 fused predict/acquisition kernel writing mu, var and acq for every candidate, the top-q
@@ -54,13 +56,13 @@ PEAK_HBM_GBPS = 8000.0
 # BASELINE.json configs (SURVEY.md §8 table / §8d synthetic inputs).  C3 is the headline
 # (the default); C2 / C4 / C5 are selectable with --config for their own timings.
 CONFIGS = {
-    "C2": dict(dim=2, n_obj=2, n_train=128, side=512, ls=20.0, q=3, kind="grid", scaling="weak",
+    "C2": dict(dim=2, n_obj=2, n_train=128, side=512, ls=20.0, q=3, kind="grid",
                workload="C2: 2D/2-obj toy_function, N_train=128, N_cand=262,144 per GPU ('ij' grid), UCB + Sigma-UCB, q=3"),
-    "C3": dict(dim=2, n_obj=2, n_train=512, side=1024, ls=20.0, q=3, kind="grid", scaling="weak",
+    "C3": dict(dim=2, n_obj=2, n_train=512, side=1024, ls=20.0, q=3, kind="grid",
                workload="C3: 2D/2-obj toy_function, N_train=512, N_cand=1,048,576 per GPU ('ij' integer grid), HVI (Sigma-UCB), q=3"),
-    "C4": dict(dim=6, n_obj=3, n_train=1024, m=1 << 21, ls=40.0, q=3, kind="sobol", scaling="strong",
+    "C4": dict(dim=6, n_obj=3, n_train=1024, m=1 << 21, ls=40.0, q=3, kind="sobol",
                workload="C4: 6D/3-obj toy_function_3d, N_train=1024, N_cand=2,097,152 unscrambled Sobol in [0,300)^6 sharded over the GPUs, HVI (Sigma-UCB), q=3"),
-    "C5": dict(dim=6, n_obj=3, n_train=2048, m=1 << 22, ls=40.0, q=16, kind="sobol", scaling="strong",
+    "C5": dict(dim=6, n_obj=3, n_train=2048, m=1 << 22, ls=40.0, q=16, kind="sobol",
                workload="C5: 6D/3-obj toy_function_3d, N_train=2048, N_cand=4,194,304 unscrambled Sobol in [0,300)^6 sharded over the GPUs, HVI (Sigma-UCB), q=16"),
 }
 BETA = 2.0
@@ -321,6 +323,9 @@ def main():
                     help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved); "
                          "fp32 = the same form on the f32 matrix cores; default: fp32 for C5 (BASELINE: "
                          "'8xMI355X fp32 with fp64 reference check'), auto otherwise")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default=None,
+                    help="strong (default): the config's fixed candidate set split over the GPUs; "
+                         "weak (grid configs): every GPU scores a full-size grid block")
     ap.add_argument("--acq", choices=("sum_ucb", "hvi"), default="sum_ucb",
                     help="sum_ucb = the reference's 'hypervolume improvement' (sum of UCBs, fused top-q); "
                          "hvi = exact hypervolume improvement over the evaluated Pareto front (extension)")
@@ -351,9 +356,18 @@ def main():
     from bayesopt_smart_amd.distributed import shard_range
     lib = bo._lib.load()
 
-    x, y, pm, pv, ls, betas, kinv, cand = make_config_problem(cfg, world)
+    scaling = args.scaling or "strong"
+    if scaling == "weak" and cfg["kind"] != "grid":
+        raise SystemExit("--scaling weak applies to the grid configs (C2/C3)")
+    x, y, pm, pv, ls, betas, kinv, cand = make_config_problem(cfg, world if scaling == "weak" else 1)
     n_obj, q = cfg["n_obj"], cfg["q"]
-    if cand[0] == "grid":
+    if cand[0] == "grid" and scaling == "strong":
+        # strong scaling: the fixed side x side grid split into P balanced contiguous index ranges
+        side = cand[2]
+        cands = bo.CandidateSet.grid([(0, cand[1]), (0, side)])
+        total = cands.n
+        offset, per_rank = shard_range(total, rank, world)
+    elif cand[0] == "grid":
         # weak scaling: rank r owns grid rows [side r, side (r + 1)) of a (side P) x side grid
         side = cand[2]
         cands = bo.CandidateSet.grid([(0, cand[1]), (0, side)])
@@ -513,14 +527,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": t_step * 1e3,
             "higher_is_better": True,
-            "scaling": cfg["scaling"],
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32" if args.mode == "fp32" else "f64",
             "data": ("synthetic (toy_function on a seeded design)" if cand[0] == "grid" else
                      "synthetic (toy_function_3d on a seeded design drawn from the Sobol set)"),
             "config": {"workload": cfg["workload"], "n_train": n, "n_cand_per_gpu": per_rank,
                        "n_cand_total": total, "n_objectives": n_obj, "dim": d, "topq": q,
-                       "parallelism": f"candidate-shard x{world}", "step_launch": step_launch},
+                       "parallelism": f"candidate-shard x{world}", "step_launch": step_launch,
+                       "candidate_offset": offset},
             "roofline": {"bound": "mfma", "achieved": executed, "peak": peak, "unit": "TFLOP/s",
                          "frac": executed / peak,
                          "flops_basis": f"executed MFMA flops per candidate ({fx}; "

@@ -184,3 +184,29 @@ def test_graphed_prepared_call_equals_direct(bo, kind):
     for k in ("mu", "acq", "top_idx"):
         np.testing.assert_array_equal(res[k].cpu().numpy(), ref2[k], err_msg=k)
     assert not np.array_equal(ref2["mu"], ref["mu"])
+
+
+def test_sharded_predict_acquire_device_path_single_rank(bo):
+    """distributed.sharded_predict_acquire on the device (no scorer) with device='cuda' (an
+    unindexed device string): one rank scores the whole set and selects what predict_acquire
+    selects; its outputs land in the caller's `out` buffers."""
+    import torch
+    from bayesopt_smart_amd.distributed import sharded_predict_acquire
+    rng = np.random.default_rng(21)
+    side, n = 128, 64
+    lin = rng.choice(side * side, size=n, replace=False)
+    x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+    y = toy_function(x)
+    pm, pv = y.mean(0), y.var(0)
+    ls, betas = np.full(2, 9.0), np.full(2, 2.0)
+    km = np.zeros((2, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    kinv = O.invert_k(n, km)
+    cands = bo.CandidateSet.grid([(0, side), (0, side)])
+    out = {"acq": torch.empty(side * side, dtype=torch.float64, device="cuda")}
+    r, (gv, gi) = sharded_predict_acquire(x, y, kinv, cands, pm, pv, ls, betas, 5, outputs=("acq",),
+                                          device="cuda", out=out)
+    ref = bo.predict_acquire(x, y, kinv, cands, pm, pv, ls, betas, outputs=("acq",), topq=5)
+    np.testing.assert_array_equal(gi, ref["top_idx"].cpu().numpy())
+    np.testing.assert_array_equal(out["acq"].cpu().numpy(), ref["acq"].cpu().numpy())
+    assert r["acq"].data_ptr() == out["acq"].data_ptr()
