@@ -209,47 +209,71 @@ def selection_check(sel_idx, cpu_acq, excluded, q):
     return True
 
 
-def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, budget_s=20.0, chunk=32768,
-                 max_cand=SIDE * SIDE):
+def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, max_cand=SIDE * SIDE, chunk=32768,
+                 passes=5, pass_s=3.0, full_limit=1 << 21):
     """Reference algorithm on the host cores: oracle/cpu_ref.c, the C/OpenMP restatement of
     update_k_star -> update_mean -> update_variance (materialised K* per candidate block,
     DGEMM K^-1 K*, the serial quadratic form) -> standardise -> UCB -> Sigma-UCB, then
     select_next_batch's full descending sort + exclusion walk.
-    points(lo, hi) -> f64 [hi - lo, d] candidates of the workload."""
+    points(lo, hi) -> f64 [hi - lo, d] candidates of the workload.
+
+    Timing: one untimed warm-up chunk, then `passes` timed passes over a
+    sample of the first S candidates (S sized for ~pass_s seconds per pass, at most the shard);
+    value = S / median pass time.  For the parity fields the rest of the shard is then scored
+    untimed when it has at most `full_limit` candidates (all of C2/C3/C4; --cpu-full for C5)."""
     from oracle import cpu_ref
     threads, share = host_cpu_share()
     cpu_ref.load()
-    done = 0
-    acqs = []
+    run = lambda lo, hi: cpu_ref.predict_acquire(x, y, points(lo, hi), kinv, pm, pv, ls, betas,  # noqa: E731
+                                                 threads=threads, outputs=True)["acq"]
+    w = min(chunk, max_cand)
     t0 = time.perf_counter()
-    while done < max_cand and time.perf_counter() - t0 < budget_s:
-        hi = min(done + chunk, max_cand)
-        acqs.append(cpu_ref.predict_acquire(x, y, points(done, hi), kinv, pm, pv, ls, betas,
-                                            threads=threads, outputs=True)["acq"])
-        done = hi
-    acq = np.concatenate(acqs)
+    run(0, w)                                            # warm-up (thread pool, BLAS)
+    rate = w / max(time.perf_counter() - t0, 1e-9)
+    sample = int(min(max_cand, max(w, (rate * pass_s) // chunk * chunk)))
+    times, acq = [], None
+    for _ in range(passes):
+        t0 = time.perf_counter()
+        acq = np.concatenate([run(lo, min(lo + chunk, sample)) for lo in range(0, sample, chunk)])
+        times.append(time.perf_counter() - t0)
+    t_med = float(np.median(times))
+    done = sample
+    if sample < max_cand and max_cand <= full_limit:     # untimed: the rest, for the parity fields
+        acq = np.concatenate([acq] + [run(lo, min(lo + chunk, max_cand)) for lo in range(sample, max_cand, chunk)])
+        done = max_cand
     cpu_sel = cpu_ref.select(acq, points(0, done), x, q)
-    dt = time.perf_counter() - t0
-    res = {"value": done / dt, "unit": "candidate-points/sec", "cores": threads, "kind": "port",
-           "sample": f"{'all' if done == max_cand else 'first'} {done} candidates of the {label} "
-                     f"(N_train={x.shape[0]}, {len(pm)} objectives, mu/var/acq written, top-{q} select), "
-                     f"oracle/cpu_ref.c (C/OpenMP, DGEMM: {cpu_ref.dgemm_name()}), {share}, {dt:.1f} s"}
+    res = {"value": sample / t_med, "unit": "candidate-points/sec", "cores": threads, "kind": "port",
+           "sample": f"{'all' if sample == max_cand else 'first'} {sample} candidates of the {label} "
+                     f"(N_train={x.shape[0]}, {len(pm)} objectives, mu/var/acq written), median of {passes} "
+                     f"timed passes ({', '.join(f'{t:.2f}' for t in times)} s) after a {w}-candidate warm-up; "
+                     f"oracle/cpu_ref.c (C/OpenMP, DGEMM: {cpu_ref.dgemm_name()}), {share}; "
+                     f"{done} candidates scored for the parity fields"}
     return res, acq, cpu_sel
 
 
+def _lib_sha256():
+    """sha256 of the loaded libbo_amd.so (the binary a PMC summary must come from)."""
+    import hashlib
+    from bayesopt_smart_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
+
+
 def pmc_traffic(workload="C3"):
-    """HBM bytes per fused-kernel launch from the newest committed rocprofv3 PMC summary of this
-    workload (profiles/*pmc*.json, scripts/pmc_summary.py), if any."""
+    """HBM bytes per fused-kernel launch from a committed rocprofv3 PMC summary of this workload
+    (profiles/*pmc*.json, scripts/pmc_summary.py) taken with THIS libbo_amd.so (its lib_sha256);
+    None when no summary of this binary exists (a summary of another build is never used)."""
+    sha = _lib_sha256()
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     for f in reversed(files):
         try:
             with open(f) as fh:
                 d = json.load(fh)
-            if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
-                return float(d["hbm_bytes_per_launch"])
+            if d.get("workload") == workload and d.get("hbm_bytes_per_launch") and d.get("lib_sha256") == sha:
+                return float(d["hbm_bytes_per_launch"]), os.path.basename(f)
         except Exception:
             pass
-    return None
+    return None, None
 
 
 def run_fit(cfg, label, dev):
@@ -316,6 +340,9 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="C3",
                     help="BASELINE.json config (C3 = the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="score the whole shard on the CPU for the parity fields even above 2^21 "
+                         "candidates (C5: minutes of host time, outside the timed region)")
     ap.add_argument("--no-graph", action="store_true", help="launch the step's kernels directly "
                     "instead of replaying them as one HIP graph")
     ap.add_argument("--fit", action="store_true", help="time the device GP fit instead (SURVEY §8f)")
@@ -517,7 +544,10 @@ def main():
         # algorithmic HBM bytes per candidate: outputs written (+ explicit coordinates read)
         n_out = sum(1 if k == "acq" else n_obj for k in outputs)
         alg_bytes = (8 * n_out + (0 if cand[0] == "grid" else 8 * d)) * per_rank
-        traffic = pmc_traffic(args.config) if args.mode == "auto" and args.acq == "sum_ucb" else None
+        # the PMC summary key: the config in its default precision, "-<mode>" otherwise
+        pmc_key = args.config if args.mode == ("fp32" if args.config == "C5" else "auto") \
+            else f"{args.config}-{args.mode}"
+        traffic, traffic_src = pmc_traffic(pmc_key) if args.acq == "sum_ucb" else (None, None)
         res = {
             "metric": metric,
             "value": total / t_step,
@@ -541,6 +571,7 @@ def main():
                          "flops_basis": f"executed MFMA flops per candidate ({fx}; "
                                         f"{'upper form' if args.mode != 'dense' else 'dense form'})",
                          "traffic": traffic,
+                         "traffic_source": traffic_src or "no PMC summary of this libbo_amd.so build",
                          "algorithmic_bytes": alg_bytes,
                          "traffic_ratio": (traffic / alg_bytes) if traffic else None,
                          "kernel": (f"cm32_predict_kernel<{2 if d <= 2 else 6}>" if args.mode == "fp32" else
@@ -584,7 +615,8 @@ def main():
                     return cands.points(np.arange(lo, hi))
                 label = f"{args.config} Sobol set"
             cb, cpu_acq, cpu_sel = cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q,
-                                                max_cand=per_rank)
+                                                max_cand=per_rank,
+                                                full_limit=per_rank if args.cpu_full else 1 << 21)
             res["cpu_baseline"] = cb
             # parity of the timed run's own outputs against the CPU reference (outside the timing)
             done = cpu_acq.size

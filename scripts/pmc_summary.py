@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "cm_predict_kernel"
+KERNEL = os.environ.get("PMC_KERNEL", "predict_kernel")   # cm_ (f64) and cm32_ (f32) fused kernels
 
 
 def main(src, dst, workload="C3", alg_bytes=40 * 1048576, kernel_label="cm_predict_kernel<2, true, true>"):
@@ -31,7 +31,12 @@ def main(src, dst, workload="C3", alg_bytes=40 * 1048576, kernel_label="cm_predi
                 for k, v in d.items():
                     vals[k].append(v)
     mean = {k: sum(v) / len(v) for k, v in vals.items()}
-    out = {"workload": workload, "kernel": kernel_label,
+    import hashlib
+    lib = os.environ.get("BO_AMD_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "bayesopt_smart_amd", "libbo_amd.so"))
+    with open(lib, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
+    out = {"workload": workload, "kernel": kernel_label, "lib_sha256": lib_sha,
            "counters_per_launch": mean, "launches_per_counter": {k: len(v) for k, v in vals.items()}}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         fetch = 2.0 * mean["FETCH_SIZE"] * 1024.0       # gfx950 16-B-read correction

@@ -1,7 +1,7 @@
 """Full-size CPU reference arrays for the -m gpu parity tests.
 
 Every candidate of a BASELINE config (C2 262,144 / C3 1,048,576 / C4 2,097,152 / C5's 2^18
-prefix) is scored by oracle/cpu_ref.c -- the C/OpenMP restatement of the reference chain
+prefix and its 8-GPU shards 0 and 7, 524,288 each) is scored by oracle/cpu_ref.c -- the C/OpenMP restatement of the reference chain
 update_k_star -> update_mean -> update_variance -> standardize_objectives -> update_ucb ->
 update_hypervolume_improvement (bayesopt/numba_kernels.py:406-570, bayesopt/acquisition.py:33-108),
 pinned to the reference's own outputs by tests/test_oracle_golden.py::test_cpu_ref_matches_oracle.

@@ -40,9 +40,10 @@ def check_predict(got, ref, pv):
         assert not bad.any(), _fail(name, bad, g, r)
 
 
-def check_topq(got_idx, acq_ref, excluded, q):
+def check_topq(got_idx, acq_ref, excluded, q, tol=None):
     """got_idx: selected global indices (in order); acq_ref: reference acq over all
-    candidates; excluded: bool mask of evaluated candidates."""
+    candidates; excluded: bool mask of evaluated candidates; tol: per-candidate acq tolerance
+    (array over all candidates, or a scalar) replacing RTOL * max(1, |ref|) (the fp32 kernel)."""
     got_idx = np.asarray(got_idx, dtype=np.int64)
     got_idx = got_idx[got_idx >= 0]
     a = np.where(excluded, -np.inf, np.asarray(acq_ref, dtype=np.float64))
@@ -51,7 +52,11 @@ def check_topq(got_idx, acq_ref, excluded, q):
     assert not excluded[got_idx].any(), "selected an evaluated point"
     order = np.argsort(-a, kind="stable")[: q + 1]
     ref_top = a[order]
-    tol = RTOL * np.maximum(1.0, np.abs(ref_top))
+    if tol is None:
+        tol = RTOL * np.maximum(1.0, np.abs(ref_top))
+    else:   # the larger of the two candidates' bounds: the chosen one and the rank's reference one
+        tv = np.broadcast_to(np.asarray(tol, dtype=np.float64), a.shape)
+        tol = np.maximum(tv[order], np.max(tv[got_idx]) if got_idx.size else 0.0)
     for t in range(got_idx.size):
         gap_ok = t + 1 < ref_top.size and (ref_top[t] - ref_top[t + 1]) > 10 * tol[t] and \
             (t == 0 or (ref_top[t - 1] - ref_top[t]) > 10 * tol[t])
