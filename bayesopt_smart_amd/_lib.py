@@ -96,6 +96,7 @@ _SIGS = {
     "bo_box_volume_sum": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_dbl_p, c_vp, c_vp]),
     "bo_invert_k": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, C.c_size_t, c_vp]),
     "bo_invert_k_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
+    "bo_invert_k_path_counts": (C.c_int, [C.POINTER(C.c_int64)]),
     "bo_compute_mll": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,
                                  C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, c_vp, C.c_size_t,
                                  c_vp]),
@@ -148,6 +149,13 @@ def check(status, what):
     if status in (ERR_NOT_PD, ERR_SINGULAR):
         raise np.linalg.LinAlgError(status_string(status))
     raise BoNativeError(status, what)
+
+
+def invert_k_path_counts():
+    """{'cholesky', 'lu', 'gauss_jordan'}: per-objective counts of bo_invert_k's paths so far."""
+    arr = (C.c_int64 * 3)()
+    check(load().bo_invert_k_path_counts(arr), "bo_invert_k_path_counts")
+    return {"cholesky": arr[0], "lu": arr[1], "gauss_jordan": arr[2]}
 
 
 def dbl_array(values, n=None):

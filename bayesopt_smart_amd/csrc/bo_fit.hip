@@ -688,6 +688,9 @@ int fit_factor(double* A, const Geo& g, const double* km, long long ld, const do
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
 }
 
+// how often each inverse path ran (per objective; bo_invert_k_path_counts)
+long long g_inv_paths[3];     // Cholesky, blocked LU, Gauss-Jordan
+
 // pinned staging for the per-call read-back (one per host thread)
 void* pinned(size_t bytes) {
   thread_local void* buf = nullptr;
@@ -709,8 +712,9 @@ extern "C" {
 size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n) {
   if (n_obj < 1 || n < 1) return 0;
   const Geo g = make_geo((int)n, n_obj, true);
-  const size_t lu = 2 * a256((size_t)n * n * sizeof(double)) + 2 * a256((size_t)n * sizeof(int));
-  return geo_bytes(g) + lu + 512;
+  // Gauss-Jordan scratch only above the blocked LU's capacity (the LU reuses the augmented region)
+  const size_t lu = n > bo_lu_max_n() ? 2 * a256((size_t)n * n * sizeof(double)) : 0;
+  return geo_bytes(g) + lu + 2 * a256((size_t)n * sizeof(int)) + 512;
 }
 
 int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_t n, void* ws,
@@ -723,11 +727,12 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
   char* w = (char*)ws;
   double* A = (double*)w;
   char* lu = w + geo_bytes(g);
+  const size_t gj = n > bo_lu_max_n() ? a256((size_t)n * n * sizeof(double)) : 0;
   double* bufA = (double*)lu;
-  double* bufB = (double*)(lu + a256((size_t)n * n * sizeof(double)));
-  int* piv = (int*)(lu + 2 * a256((size_t)n * n * sizeof(double)));
+  double* bufB = (double*)(lu + gj);
+  int* piv = (int*)(lu + 2 * gj);
   int* perm = piv + a256((size_t)n * sizeof(int)) / sizeof(int);
-  int* status = (int*)(lu + 2 * a256((size_t)n * n * sizeof(double)) + 2 * a256((size_t)n * sizeof(int)));
+  int* status = (int*)(lu + 2 * gj + 2 * a256((size_t)n * sizeof(int)));
   BO_CHECK_HIP(hipMemsetAsync(status, 0, 256, s));
   FitParams p;
   memset(&p, 0, sizeof(p));
@@ -742,10 +747,23 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
   BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * n_obj, hipMemcpyDeviceToHost, s));
   BO_CHECK_HIP(hipStreamSynchronize(s));
   int fail[BO_MAX_OBJ];
-  for (int o = 0; o < n_obj; ++o) fail[o] = hstat[o];
-  // LU fallback (Gauss-Jordan, partial pivoting) for the objectives whose Cholesky failed
+  for (int o = 0; o < n_obj; ++o) {
+    fail[o] = hstat[o];
+    if (!fail[o]) __atomic_fetch_add(&g_inv_paths[0], 1, __ATOMIC_RELAXED);
+  }
+  // LU path for the objectives whose Cholesky failed or whose K is not symmetric: the blocked
+  // LU with partial pivoting of bo_lu.hip in the (now free) augmented-matrix region; Gauss-Jordan
+  // with partial pivoting above its register capacity (N > 2048)
   for (int o = 0; o < n_obj; ++o) {
     if (!fail[o]) continue;
+    if (n <= bo_lu_max_n() && geo_bytes(g) >= bo_lu_workspace_size(n)) {
+      const double* ko = km + (long long)o * ld * ld;
+      const int st2 = bo_lu_inverse(out + (long long)o * n * n, ko, ld, n, A, geo_bytes(g), s);
+      __atomic_fetch_add(&g_inv_paths[1], 1, __ATOMIC_RELAXED);
+      if (st2 != BO_OK) return st2;
+      continue;
+    }
+    __atomic_fetch_add(&g_inv_paths[2], 1, __ATOMIC_RELAXED);
     int* gstat = status + BO_MAX_OBJ + 1;
     BO_CHECK_HIP(hipMemsetAsync(gstat, 0, sizeof(int), s));
     const long long total = (long long)n * n;
@@ -787,22 +805,11 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
   return BO_OK;
 }
 
-#ifdef BO_FIT_TIMING
-// diagnostic build only: the phase stamps of the step launches since the last call (pairs of
-// (k << 16 | block << 4 | tag, 100 MHz clock)); returns the count and resets it
-int bo_debug_fit_timing(long long* out, int cap) {
-  int cnt = 0;
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(bo_fit_tcount), sizeof(int)) != hipSuccess) return -1;
-  if (cnt > 4096) cnt = 4096;
-  if (cnt > cap) cnt = cap;
-  if (cnt > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_fit_tstamp), sizeof(long long) * 2 * cnt) != hipSuccess)
-    return -1;
-  const int zero = 0;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(bo_fit_tcount), &zero, sizeof(int)) != hipSuccess) return -1;
-  return cnt;
+int bo_invert_k_path_counts(int64_t* counts) {
+  if (!counts) return BO_ERR_ARG;
+  for (int i = 0; i < 3; ++i) counts[i] = __atomic_load_n(&g_inv_paths[i], __ATOMIC_RELAXED);
+  return BO_OK;
 }
-#endif
 
 size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n) {
   if (n_obj < 1 || n < 1) return 0;

@@ -313,6 +313,17 @@ def run_fit(cfg, label, dev):
     mll_ms, mll = timed(mll_fn, 10)
     km_h = np.zeros((n_obj, n, n))
     mll_ref = O.compute_mll(x, y, km_h, pm, pv, ls, n)
+    # the LU path (bo_lu.hip): objective 0's K made non-symmetric forces it (Cholesky skipped)
+    rng = np.random.default_rng(3)
+    km_lu = km.clone()
+    km_lu[0] += torch.tensor(np.triu(rng.uniform(-1e-3, 1e-3, size=(n, n)) * pv[0], 1), device=dev)
+    lu_fn = lambda: bo.kernels.invert_k(n, km_lu)  # noqa: E731
+    c0 = bo._lib.invert_k_path_counts()
+    lu_fn()
+    lu_ms, kinv_lu = timed(lu_fn, 3)
+    c1 = bo._lib.invert_k_path_counts()
+    ref_lu = np.linalg.inv(km_lu[0].cpu().numpy() + 1e-6 * np.eye(n))
+    lu_err = float(np.abs(kinv_lu[0].cpu().numpy() - ref_lu).max() / np.abs(ref_lu).max())
     ls_fit, pv_fit = ls.copy(), pv.copy()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -325,11 +336,45 @@ def run_fit(cfg, label, dev):
         "n_gpus": 1, "dtype": "f64", "data": "synthetic (the bench workload's training set)",
         "config": {"workload": cfg["workload"], "n_train": n, "n_objectives": n_obj, "dim": x.shape[1]},
         "update_k_invert_k_ms": inv_ms, "invert_k_rel_err_vs_lapack": inv_err,
+        "invert_k_lu_path_ms": lu_ms, "invert_k_lu_path_rel_err_vs_lapack": lu_err,
+        "invert_k_lu_path_note": (f"objective 0 non-symmetric -> blocked LU + getrs; objective 1 "
+                                  f"Cholesky; paths taken per timed call: "
+                                  f"{ {k: (c1[k] - c0[k]) / 4 for k in c1} }"),
         "compute_mll_ms": mll_ms, "mll": mll, "mll_lapack": mll_ref,
         "mll_rel_err": abs(mll - mll_ref) / max(1.0, abs(mll_ref)),
         "powell_nfev": int(res.nfev), "powell_ms_per_eval": fit_ms / max(int(res.nfev), 1),
         "fitted_length_scales": ls_fit.tolist(),
     }
+
+
+def run_fit_demo(n_max, dev):
+    """--fit-demo: how often invert_k leaves the Cholesky path in a headless demo-style run
+    (examples/demo_2d.py: toy_function on the 300 x 300 grid, 6 initial points, batches of 3,
+    hyper-parameters Powell-fitted every iteration as the reference's loop does,
+    bayesian_optimization.py:115-123) up to N = n_max training points."""
+    import bayesopt_smart_amd as bo
+
+    def toy(p):
+        p = np.asarray(p, dtype=np.float64)
+        return np.array([-((p[0] - 150) ** 2) + 100.0, -((p[1] - 150) ** 2) + 20.0])
+
+    iters = (n_max - 6) // 3
+    c0 = bo._lib.invert_k_path_counts()
+    t0 = time.perf_counter()
+    opt = bo.BayesianOptimization(toy, [(0, 300), (0, 300)], n_objectives=2, n_iterations=iters,
+                                  initial_samples=6, batch_size=3, device=dev)
+    opt.optimize()
+    dt = time.perf_counter() - t0
+    c1 = bo._lib.invert_k_path_counts()
+    d = {k: c1[k] - c0[k] for k in c1}
+    tot = sum(d.values())
+    return {"metric": "invert_k path frequency in a demo-style run (Powell-fitted hyper-parameters)",
+            "value": d["lu"] + d["gauss_jordan"], "unit": f"objective inversions off the Cholesky path (of {tot})",
+            "higher_is_better": False, "n_gpus": 1, "data": "toy_function on the 300 x 300 grid",
+            "config": {"initial_samples": 6, "batch_size": 3, "iterations": iters, "n_train_final": 6 + 3 * iters},
+            "paths": d, "fallback_fraction": (d["lu"] + d["gauss_jordan"]) / max(tot, 1),
+            "fitted_length_scales": opt.length_scales.tolist(), "run_s": dt,
+            "best_found": opt.x_vector[np.argmax(opt.y_vector[: opt.n_evaluations, 0])].tolist()}
 
 
 def main():
@@ -346,6 +391,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch the step's kernels directly "
                     "instead of replaying them as one HIP graph")
     ap.add_argument("--fit", action="store_true", help="time the device GP fit instead (SURVEY §8f)")
+    ap.add_argument("--fit-demo", type=int, default=0, metavar="N_MAX",
+                    help="count invert_k's Cholesky / LU paths in a demo-style run up to N_MAX points")
     ap.add_argument("--mode", choices=("auto", "dense", "fp32"), default=None,
                     help="variance formulation (auto = 2 k.(U k) with U = triu(sym(K^-1)), diagonal halved); "
                          "fp32 = the same form on the f32 matrix cores; default: fp32 for C5 (BASELINE: "
@@ -371,10 +418,11 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if args.fit:
+    if args.fit or args.fit_demo:
         if world > 1:
-            raise SystemExit("--fit is a single-GPU measurement")
-        print(json.dumps(run_fit(cfg, args.config, dev)), flush=True)
+            raise SystemExit("--fit / --fit-demo are single-GPU measurements")
+        print(json.dumps(run_fit_demo(args.fit_demo, dev) if args.fit_demo else run_fit(cfg, args.config, dev)),
+              flush=True)
         return
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)

@@ -252,12 +252,19 @@ int bo_hypervolume_improvement_exact(double* acq, const double* ucb, int64_t ld,
  * GP fit on device.
  * ---------------------------------------------------------------------------------- */
 
-/* invert_k  bayesopt/numba_kernels.py:370-403: out[o] = inv(K[o][:N,:N] + 1e-6 I) by LU with
- * partial pivoting (LAPACK gesv semantics).  kernel_matrix device [n_obj][ld][ld];
+/* invert_k  bayesopt/numba_kernels.py:370-403: out[o] = inv(K[o][:N,:N] + 1e-6 I) (the
+ * reference's LAPACK gesv with the identity): a blocked Cholesky when K is symmetric, the blocked
+ * LU with partial pivoting (getrf's row choice) + getrs when the Cholesky fails or K is not
+ * symmetric.  kernel_matrix device [n_obj][ld][ld];
  * out device [n_obj][n][n]. Returns BO_ERR_SINGULAR on an exactly singular pivot.
  * Synchronous (the status depends on the factorisation). */
 int bo_invert_k(double* out, const double* kernel_matrix, int64_t ld, int32_t n_obj, int64_t n,
                 void* workspace, size_t workspace_bytes, void* stream);
+/* Per-objective counts of the paths bo_invert_k took since the library was loaded (process-wide,
+ * host counters): counts[0] Cholesky, [1] blocked LU (Cholesky failed or K not symmetric;
+ * N <= 2048), [2] Gauss-Jordan (the same above N = 2048).  Diagnostics for the fallback's
+ * frequency. */
+int bo_invert_k_path_counts(int64_t* counts);
 size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n);
 
 /* compute_mll  bayesopt/numba_kernels.py:152-235 (Gram rebuilt into kernel_matrix first, as

@@ -315,3 +315,49 @@ def test_demo_trajectory_replay_each_iteration(bo, it):
             assert sel[t] == ridx[t], (it, t, sel[t], ridx[t])
         else:
             assert abs(acq[sel[t]] - rval[t]) <= 2 * tt, (it, t)
+
+
+@pytest.mark.parametrize("n", [512, 2048])
+def test_invert_k_lu_path_matches_lapack(bo, n):
+    """invert_k's blocked LU path (bo_lu.hip: getrf partial pivoting + getrs with the identity,
+    numba_kernels.py:401) at the C3 and C5 N: objective 0's K is made non-symmetric (the Cholesky
+    is then not taken), objective 1 stays symmetric (Cholesky); both against LAPACK's inv."""
+    import torch
+    rng = np.random.default_rng(n)
+    x = rng.uniform(0, 300, size=(n, 2))
+    pv, ls = np.array([3e3, 5e2]), np.array([25.0, 40.0])
+    km = np.zeros((2, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    km[0] += np.triu(rng.uniform(-1e-3, 1e-3, size=(n, n)) * pv[0], 1)   # not symmetric
+    before = bo._lib.invert_k_path_counts()
+    got = bo.kernels.invert_k(n, torch.tensor(km, device="cuda")).cpu().numpy()
+    after = bo._lib.invert_k_path_counts()
+    assert after["lu"] - before["lu"] == 1 and after["cholesky"] - before["cholesky"] == 1
+    ref = O.invert_k(n, km)
+    for o in range(2):
+        cond = np.linalg.cond(km[o] + 1e-6 * np.eye(n))
+        scale = np.abs(ref[o]).max()
+        assert np.abs(got[o] - ref[o]).max() <= 1e-13 * cond * scale, (o, cond)
+
+
+def test_invert_k_lu_path_ill_conditioned(bo):
+    """The regime that makes the Cholesky fail (Powell-fitted length scales drive
+    cond(K + 1e-6 I) to 1e14..1e18; the reference's inv still returns): the LU path returns a
+    finite inverse whose residual |(K + 1e-6 I) X - I| is at LAPACK's level for that condition."""
+    rng = np.random.default_rng(4)
+    n = 300
+    x = rng.uniform(0, 300, size=(n, 2))
+    pv, ls = np.array([2e9]), np.array([400.0])
+    km = np.zeros((1, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    a = km[0] + 1e-6 * np.eye(n)
+    before = bo._lib.invert_k_path_counts()
+    got = bo.kernels.invert_k(n, km)[0]
+    after = bo._lib.invert_k_path_counts()
+    ref = np.linalg.inv(a)
+    assert np.isfinite(got).all()
+    res_got = np.abs(a @ got - np.eye(n)).max()
+    res_ref = np.abs(a @ ref - np.eye(n)).max()
+    print(f"cond {np.linalg.cond(a):.2e}, residual device {res_got:.3e}, LAPACK {res_ref:.3e}, paths {after}")
+    assert res_got <= max(100.0 * res_ref, 1e-6)
+    assert after["lu"] + after["cholesky"] > before["lu"] + before["cholesky"]
