@@ -10,7 +10,7 @@ contraction leaves |d std_mu| <= EPS_MU and |d std_var| <= EPS_VAR (var = pv - q
 the training points, where q ~ pv in f32); the UCB's sqrt propagates |d sqrt(v)| <=
 min(sqrt(dv), dv / sqrt(v_ref)), so candidate i's acquisition bound is
     tol_i = sum_o EPS_MU + beta_o min(sqrt(EPS_VAR), EPS_VAR / sqrt(std_var_ref[o, i]))
--- ~1e-4 away from the data, ~7e-3 at a training point (round 2 allowed 0.19 max|acq|
+-- ~4e-5 away from the data, ~1.3e-2 at a training point (round 2 allowed 0.19 max|acq|
 everywhere).  The selection is judged tie-aware with that per-candidate bound."""
 import os
 import sys
@@ -24,8 +24,8 @@ from fullref import cpu_full
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 pytestmark = pytest.mark.gpu
 
-EPS_MU = 5e-5           # |d std_mu| (f32 mean: sum of 2048 f32 products, |alpha k| ~ 1)
-EPS_VAR = 3e-5          # |d std_var| (f32 q = 2 k.(U k) against pv)
+EPS_MU = 1e-5           # |d std_mu| (f32 mean; measured 2.5e-6 on shards 0 and 7)
+EPS_VAR = 1e-5          # |d std_var| (f32 q = 2 k.(U k) against pv; measured 2.6e-6)
 WORLD, SHARDS = 8, (0, 7)
 
 
