@@ -101,6 +101,9 @@ _SIGS = {
                                  C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, c_vp, C.c_size_t,
                                  c_vp]),
     "bo_compute_mll_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
+    "bo_compute_mll_each": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,
+                                      C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, c_vp, C.c_size_t,
+                                      c_vp]),
     "bo_sobol_points": (C.c_int, [C.POINTER(SobolDesc), C.c_int32, C.POINTER(C.c_int64), C.c_int64,
                                   c_dbl_p]),
     "bo_sobol_direction_numbers": (C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_uint32)]),

@@ -128,9 +128,12 @@ __device__ __forceinline__ int tri_row(long long t) {
 // ------------------------------------------------------------------------------- init
 // Lower 32 x 32 tiles of the augmented matrix (one workgroup per tile, linear tile index over the
 // lower triangle of the K part, then the bottom tiles that are live in their column block).
-//   K part (i, j < N):  MLL: v / pv + 1e-8 d_ij with v = pv exp(-0.5 |x_i - x_j|^2 / ls^2) exactly
-//                       as update_k (numba_kernels.py:352-361), v also stored to the caller's
-//                       kernel_matrix in both triangles (compute_mll rebuilds it, :178-185);
+//   K part (i, j < N):  MLL: e + 1e-8 d_ij with e = exp(-0.5 |x_i - x_j|^2 / ls^2), the
+//                       correlation matrix K / pv of :195-198 (the reference's (pv e) / pv, within
+//                       an ulp: the value depends on ls only, so per-objective MLLs memoise
+//                       across Powell's pv moves), and pv e -- update_k's value
+//                       (numba_kernels.py:352-361) -- stored to the caller's kernel_matrix in
+//                       both triangles (compute_mll rebuilds it, :178-185);
 //                       inverse: K[i][j] + 1e-6 d_ij from the caller's kernel_matrix, with
 //                       K[i][j] == K[j][i] checked (an asymmetric K takes the LU path);
 //   K padding:          identity;
@@ -203,8 +206,8 @@ __global__ __launch_bounds__(256) void fit_init_kernel(double* __restrict__ A, G
             const double d = x[i * dim + k] - x[j * dim + k];
             sq = __builtin_fma(d, d, sq);
           }
-          v = p.pv[o] * exp(-0.5 * sq / p.ls2[o]);
-          ko[i * ld + j] = v;                   // row i of the caller's matrix
+          v = exp(-0.5 * sq / p.ls2[o]);        // K / pv, the correlation matrix of :195-198
+          ko[i * ld + j] = p.pv[o] * v;         // row i of the caller's matrix (update_k's value)
         }
         tile[rr][cc] = v;
       }
@@ -214,7 +217,7 @@ __global__ __launch_bounds__(256) void fit_init_kernel(double* __restrict__ A, G
         for (int e = tid; e < NB * NB; e += 256) {
           const int rr = e >> 5, cc = e & 31;   // row c0 + rr, column r0 + cc
           const long long i = c0 + rr, j = r0 + cc;
-          if (i < g.n && j < g.n) ko2[i * ld + j] = tile[cc][rr];
+          if (i < g.n && j < g.n) ko2[i * ld + j] = p.pv[o] * tile[cc][rr];
         }
       }
     } else {
@@ -248,7 +251,6 @@ __global__ __launch_bounds__(256) void fit_init_kernel(double* __restrict__ A, G
       if (asym) atomicOr(status + o, 2);
     }
     __syncthreads();
-    const double scale = g.ident ? 1.0 : p.pv[o];
 #pragma unroll
     for (int pass = 0; pass < NB / 8; ++pass) {
       const int cc = c + 8 * pass;
@@ -256,8 +258,7 @@ __global__ __launch_bounds__(256) void fit_init_kernel(double* __restrict__ A, G
       if (i < j) continue;
       double v;
       if (i < g.n && j < g.n) {
-        const double kv = tile[r][cc];
-        v = (g.ident ? kv : kv / scale) + (i == j ? p.jitter : 0.0);
+        v = tile[r][cc] + (i == j ? p.jitter : 0.0);
       } else {
         v = i == j ? 1.0 : 0.0;
       }
@@ -817,10 +818,10 @@ size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n) {
   return geo_bytes(g) + a256((size_t)n_obj * part_len(g) * sizeof(double) + BO_MAX_OBJ * sizeof(int)) + 512;
 }
 
-int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* y, int64_t ld_y,
-                   double* km, int64_t ld, int32_t n_obj, const double* pm, const double* pv,
-                   const double* ls, int64_t n, void* ws, size_t ws_bytes, void* stream) {
-  if (!mll_out || !x || !y || !km || !pm || !pv || !ls || n_obj < 1 || n_obj > BO_MAX_OBJ ||
+int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const double* y, int64_t ld_y,
+                        double* km, int64_t ld, int32_t n_obj, const double* pm, const double* pv,
+                        const double* ls, int64_t n, void* ws, size_t ws_bytes, void* stream) {
+  if (!mll_obj || !x || !y || !km || !pm || !pv || !ls || n_obj < 1 || n_obj > BO_MAX_OBJ ||
       n < 1 || ld < n || ld_y < n_obj || dim < 1)
     return BO_ERR_ARG;
   if (n > (1 << 16)) return BO_ERR_UNSUPPORTED;
@@ -850,8 +851,7 @@ int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* 
   for (int o = 0; o < n_obj; ++o)
     if (hstat[o]) return BO_ERR_NOT_PD;
   // mll_o = -0.5 yc.alpha - 0.5 log det - 0.5 N log(2 pi) (numba_kernels.py:222-232); yc.alpha =
-  // |z|^2 / var(y - pm) (unscaled when the std is 0, :206-207); np.sum over objectives (:235)
-  double tot = 0.0;
+  // |z|^2 / var(y - pm) (unscaled when the std is 0, :206-207)
   for (int o = 0; o < n_obj; ++o) {
     const double* q = h + (size_t)o * part_len(g);
     double ld_sum = 0.0, fit = 0.0;
@@ -861,8 +861,20 @@ int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* 
     }
     const double var = q[2 * g.nbt];
     if (sqrt(var) > 0.0) fit /= var;
-    tot += -0.5 * fit + (-0.5 * (2.0 * ld_sum)) + (-0.5 * (double)n * log(2.0 * 3.141592653589793));
+    mll_obj[o] = -0.5 * fit + (-0.5 * (2.0 * ld_sum)) + (-0.5 * (double)n * log(2.0 * 3.141592653589793));
   }
+  return BO_OK;
+}
+
+int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* y, int64_t ld_y,
+                   double* km, int64_t ld, int32_t n_obj, const double* pm, const double* pv,
+                   const double* ls, int64_t n, void* ws, size_t ws_bytes, void* stream) {
+  double v[BO_MAX_OBJ];
+  if (!mll_out) return BO_ERR_ARG;
+  const int st = bo_compute_mll_each(v, x, dim, y, ld_y, km, ld, n_obj, pm, pv, ls, n, ws, ws_bytes, stream);
+  if (st != BO_OK) return st;
+  double tot = 0.0;                            // np.sum over objectives (:235): sequential, < 8 terms
+  for (int o = 0; o < n_obj; ++o) tot += v[o];
   *mll_out = tot;
   return BO_OK;
 }

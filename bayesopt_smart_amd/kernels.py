@@ -155,11 +155,42 @@ def compute_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance, l
     return out.value
 
 
+def _mll_terms(xd, yd, km, prior_mean, prior_variance, length_scales, n, objs):
+    """Per-objective MLL terms (bo_compute_mll_each) of the objectives `objs` (device arrays;
+    one call over all objectives, or one single-objective call for one of them)."""
+    lib = _lib.load()
+    n_obj_all, ld = km.shape[0], km.shape[-1]
+    dev = km.device
+    if len(objs) == n_obj_all:
+        o0, cnt = 0, n_obj_all
+    else:
+        assert len(objs) == 1
+        o0, cnt = objs[0], 1
+    out = (C.c_double * cnt)()
+    ws = Workspace.get(lib.bo_compute_mll_workspace_size(cnt, n), dev)
+    sel = lambda v: _host_vec(np.asarray(v, dtype=np.float64)[o0:o0 + cnt], cnt)  # noqa: E731
+    st = lib.bo_compute_mll_each(out, xd.data_ptr(), xd.shape[1], yd.data_ptr() + 8 * o0, yd.stride(0),
+                                 km.data_ptr() + 8 * o0 * ld * ld, ld, cnt, sel(prior_mean),
+                                 sel(prior_variance), sel(length_scales), n, ws.data_ptr(), ws.numel(),
+                                 stream_handle(dev))
+    _lib.check(st, "bo_compute_mll_each")
+    return {o0 + i: out[i] for i in range(cnt)}
+
+
 def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance,
-                             length_scales, current_eval):
+                             length_scales, current_eval, memo=True):
     """numba_kernels.py:238-321 — Powell over [ls..., var...] (bounds >= 1e-5) maximising the
     device MLL; updates length_scales and prior_variance in place, returns the OptimizeResult.
-    The training arrays are staged on the device once for all ~100-200 MLL evaluations."""
+    The training arrays are staged on the device once for all ~100-200 MLL evaluations.
+
+    `memo`: the MLL is a sum of per-objective terms, each a function of (x, y, pm, ls_o) only --
+    the correlation matrix K / pv does not depend on pv (:195-198; the device builds it pv-free) --
+    and Powell moves mostly one coordinate at a time: each term is computed once per distinct
+    ls_o (bo_compute_mll_each over the objectives whose ls changed) and summed in objective order
+    like np.sum (:235).  The returned values are bit-identical to recomputing every term (the same
+    device arithmetic), so Powell's path is unchanged; evaluations that move only pv need no
+    device call (about half of them).  kernel_matrix ends as the reference leaves it: the Gram of
+    the last evaluated hyper-parameters."""
     dev = _dev_of(kernel_matrix, x_vector, y_vector)
     n_obj = np.asarray(length_scales).shape[0] if not isinstance(length_scales, torch.Tensor) \
         else length_scales.shape[0]
@@ -168,15 +199,33 @@ def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prio
     km = _Arg(kernel_matrix, dev, write=True)
     ls0 = length_scales.cpu().numpy() if isinstance(length_scales, torch.Tensor) else np.asarray(length_scales)
     pv0 = prior_variance.cpu().numpy() if isinstance(prior_variance, torch.Tensor) else np.asarray(prior_variance)
+    pm = np.asarray(prior_mean.cpu().numpy() if isinstance(prior_mean, torch.Tensor) else prior_mean,
+                    dtype=np.float64)
     initial_guess = np.concatenate([ls0, pv0])
     bounds = [(HYPERPARAM_MIN_BOUND, None)] * (2 * n_obj)
+    cache = [dict() for _ in range(n_obj)]
+    last = [None]
 
     def objective(params):
-        return -compute_mll(xd, yd, km.t, prior_mean, params[n_obj:], params[:n_obj], current_eval)
+        ls, pv = params[:n_obj], params[n_obj:]
+        last[0] = params.copy()
+        if not memo:
+            return -compute_mll(xd, yd, km.t, pm, pv, ls, current_eval)
+        todo = [o for o in range(n_obj) if float(ls[o]) not in cache[o]]
+        if todo:
+            objs = todo if len(todo) == 1 else list(range(n_obj))
+            for o, v in _mll_terms(xd, yd, km.t, pm, pv, ls, current_eval, objs).items():
+                cache[o][float(ls[o])] = v
+        tot = 0.0
+        for o in range(n_obj):                  # np.sum over < 8 terms: sequential (:235)
+            tot += cache[o][float(ls[o])]
+        return -tot
 
     res = minimize(objective, initial_guess, method=HYPERPARAM_METHOD, bounds=bounds,
                    options={"xtol": HYPERPARAM_XTOL, "ftol": HYPERPARAM_FTOL,
                             "maxiter": HYPERPARAM_MAXITER})
+    if memo and last[0] is not None:            # the reference's compute_mll side effect
+        update_k(km.t, xd, 0, current_eval, last[0][n_obj:], last[0][:n_obj])
     km.finish()
     _assign(length_scales, res.x[:n_obj])
     _assign(prior_variance, res.x[n_obj:])

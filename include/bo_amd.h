@@ -274,6 +274,14 @@ int bo_compute_mll(double* mll_out, const double* x, int32_t dim, const double* 
                    double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
                    const double* prior_variance, const double* length_scales,
                    int64_t current_eval, void* workspace, size_t workspace_bytes, void* stream);
+/* The per-objective terms of compute_mll: mll_obj[o] (host, [n_obj]); compute_mll is their sum in
+ * objective order.  Each term depends on (x, y[:, o], pm[o], ls[o]) only -- the correlation
+ * matrix K / pv does not depend on pv -- so a caller may memoise terms across calls (the Powell
+ * driver of bayesopt_smart_amd.kernels does).  Same arguments and errors as bo_compute_mll. */
+int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const double* y, int64_t ld_y,
+                        double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
+                        const double* prior_var, const double* length_scale, int64_t n,
+                        void* workspace, size_t workspace_bytes, void* stream);
 size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n);
 
 /* ------------------------------------------------------------------------------------

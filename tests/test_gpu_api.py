@@ -361,3 +361,28 @@ def test_invert_k_lu_path_ill_conditioned(bo):
     print(f"cond {np.linalg.cond(a):.2e}, residual device {res_got:.3e}, LAPACK {res_ref:.3e}, paths {after}")
     assert res_got <= max(100.0 * res_ref, 1e-6)
     assert after["lu"] + after["cholesky"] > before["lu"] + before["cholesky"]
+
+
+@pytest.mark.parametrize("n,dim,n_obj", [(96, 2, 2), (300, 6, 3)])
+def test_powell_memo_equals_full_evaluations(bo, n, dim, n_obj):
+    """optimize_hyperparams_mll's memoised per-objective terms (bo_compute_mll_each) return the
+    same MLL bits as recomputing every term: the same Powell path, result and evaluation count;
+    kernel_matrix ends as the Gram of the last evaluated hyper-parameters, as in the reference."""
+    import torch
+    x, y, pm, pv, ls = _sobol_problem(n, dim, n_obj, 30.0, 7)
+    xd, yd = torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda")
+    out = []
+    for memo in (False, True):
+        km = torch.zeros((n_obj, n, n), dtype=torch.float64, device="cuda")
+        lsv, pvv = ls.copy(), pv.copy()
+        r = bo.kernels.optimize_hyperparams_mll(xd, yd, km, pm, pvv, lsv, n, memo=memo)
+        out.append((r.x.copy(), r.nfev, r.fun, km.cpu().numpy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
+    np.testing.assert_array_equal(out[0][3], out[1][3])
+    # each term only depends on ls_o: the sum of the terms is compute_mll
+    km = torch.zeros((n_obj, n, n), dtype=torch.float64, device="cuda")
+    terms = bo.kernels._mll_terms(xd, yd, km, pm, pv, ls, n, list(range(n_obj)))
+    assert sum(terms[o] for o in range(n_obj)) == bo.kernels.compute_mll(xd, yd, km, pm, pv, ls, n)
+    one = bo.kernels._mll_terms(xd, yd, km, pm, pv * 3.0, ls, n, [n_obj - 1])
+    assert one[n_obj - 1] == terms[n_obj - 1]          # pv-free: bit-identical
