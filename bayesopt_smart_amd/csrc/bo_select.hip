@@ -233,6 +233,380 @@ __device__ __forceinline__ void wave_rank_insert(double& lv, long long& li, doub
   if (lane < q) { lv = buf[lane].v; li = buf[lane].i; }
 }
 
+// ---------------------------------------------------------------------------------------
+// Small-q selection (q <= 16), the default for those q.  One workgroup of 16 waves per CU (the
+// evaluated points' LDS hash set is built once per CU), U elements per lane, every load in
+// flight at once.  Per span of 16 x 64 U elements:
+//   * each lane sorts its U elements (order keys, best first) -- its "head" is then its best;
+//   * round 1: every wave's best non-excluded element (wave arg-best of the lane heads: DPP
+//     inside the 16-lane rows, v_readlane of the 4 row bests; the winner is probed against the
+//     evaluated points and, if it is one, its lane moves to its next element);
+//   * the q-th best of the 16 wave bests is a bound B for the workgroup: q non-excluded
+//     elements are not worse than it, so the workgroup's top-q is not worse than it; a wave
+//     whose best is worse than B is done;
+//   * the other waves extract up to q - 1 more heads strictly better than B (and than their
+//     running list's q-th), probe them in parallel and rank-insert them (wave_rank_insert);
+//     an excluded one leaves the batch short and the extraction goes on;
+//   * the 16 wave lists are ranked in LDS, 4 lists per wave and level (block_lists_merge).
+// select_merge_kernel runs the same machinery over the [blocks][q] lists (each lane one list).
+// Round-3 A/B history: a 64-lane bitonic sort of the lane bests at one wave per SIMD took 39 us
+// at C3 (q = 3) and 176 us at C5 (q = 16); q arg-best rounds in every wave of 1024 four-wave
+// workgroups, 34 / 254 us -- VALU-bound on the 64-bit key compares (an extraction round of
+// every wave cost ~2.5 us); the event kernel below: 33 / 79 us.
+// ---------------------------------------------------------------------------------------
+struct NoExcl {
+  __device__ bool operator()(long long) const { return false; }
+};
+struct SelExcl {
+  const SelArgs* a;
+  const unsigned long long* hk;
+  const int* hi;
+  unsigned int hm;
+  __device__ bool operator()(long long gi) const {
+    return a->n_excl > 0 && cand_excluded(*a, gi - a->cand_offset, hk, hi, hm);
+  }
+};
+
+// order of (key, index) pairs; valid keys are never 0 (bo_order_key), empty entries have key 0
+__device__ __forceinline__ bool kbefore(unsigned long long ka, long long ia, unsigned long long kb, long long ib) {
+  return ka > kb || (ka == kb && ia < ib);
+}
+
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), CTRL, 0xF, 0xF, false);
+  return ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
+}
+template <int CTRL>
+__device__ __forceinline__ void dpp_best_step(unsigned long long& k, long long& i) {
+  const unsigned long long ok = dpp_u64<CTRL>(k);
+  const long long oi = (long long)dpp_u64<CTRL>((unsigned long long)i);
+  const bool t = kbefore(ok, oi, k, i);
+  k = t ? ok : k;
+  i = t ? oi : i;
+}
+// The wave's best (order key, index) over the lanes' (k, i), wave-uniform: quad_perm xor 1 and
+// xor 2, row_half_mirror, row_mirror (every lane of a 16-lane row then holds the row's best),
+// then the 4 row bests by v_readlane.
+__device__ __forceinline__ void wave_argbest(unsigned long long k, long long i, unsigned long long& wk,
+                                             long long& wi) {
+  dpp_best_step<0xB1>(k, i);
+  dpp_best_step<0x4E>(k, i);
+  dpp_best_step<0x141>(k, i);
+  dpp_best_step<0x140>(k, i);
+  wk = bo_readlane_u(k, 0);
+  wi = bo_readlane_i(i, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) {
+    const unsigned long long rk = bo_readlane_u(k, r);
+    const long long ri = bo_readlane_i(i, r);
+    const bool t = kbefore(rk, ri, wk, wi);
+    wk = t ? rk : wk;
+    wi = t ? ri : wi;
+  }
+}
+
+// A lane's U entries, sorted best first, and the position of its head (the best not taken).
+template <int U>
+struct LaneRun {
+  unsigned long long k[U];
+  long long i[U];
+  int h;
+  __device__ __forceinline__ void sort() {
+    auto cx = [&](int x, int y) {
+      const bool sw = kbefore(k[y], i[y], k[x], i[x]);
+      const unsigned long long tk = k[x];
+      const long long ti = i[x];
+      k[x] = sw ? k[y] : k[x];
+      i[x] = sw ? i[y] : i[x];
+      k[y] = sw ? tk : k[y];
+      i[y] = sw ? ti : i[y];
+    };
+    if constexpr (U == 2) cx(0, 1);
+    if constexpr (U == 4) { cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2); }
+    static_assert(U == 1 || U == 2 || U == 4, "sorting network for U in {1, 2, 4}");
+  }
+  __device__ __forceinline__ void head(unsigned long long& hk, long long& hi) const {
+    hk = 0ull;
+    hi = -1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      hk = h == u ? k[u] : hk;
+      hi = h == u ? i[u] : hi;
+    }
+  }
+};
+
+// Extract this wave's entries strictly better than (bk, bi) -- and than the running list's q-th
+// -- up to q of them, excluded ones skipped, into the list (lv, li: lanes 0..q-1 sorted).  `first`
+// (wave-uniform, optional) is an entry already taken from the lanes, inserted with the batch.
+template <int U, class EX>
+__device__ __forceinline__ void wave_extract(LaneRun<U>& r, unsigned long long bk, long long bi, double& lv,
+                                             long long& li, int q, TopEntry* rbuf, const EX& excluded,
+                                             unsigned long long fk, long long fi) {
+  const int lane = threadIdx.x & 63;
+  for (;;) {
+    // the tighter of the bound and the list's q-th entry
+    const double lq = bo_readlane_d(lv, q - 1);
+    const long long lqi = bo_readlane_i(li, q - 1);
+    const unsigned long long lk = bo_order_key(lq, lqi);
+    if (kbefore(lk, lqi, bk, bi)) { bk = lk; bi = lqi; }
+    double nv = -__builtin_inf();
+    long long ni = -1;
+    int nb = 0;
+    if (fk) {                                   // the pre-taken entry (already probed)
+      if (lane == 0) { nv = bo_key_value(fk); ni = fi; }
+      nb = 1;
+      fk = 0ull;
+    }
+    const int first_new = nb;
+    for (; nb < q; ++nb) {
+      unsigned long long hk;
+      long long hi;
+      r.head(hk, hi);
+      unsigned long long wk;
+      long long wi;
+      wave_argbest(hk, hi, wk, wi);
+      if (wk == 0ull || !kbefore(wk, wi, bk, bi)) break;
+      if (hi == wi) ++r.h;                       // the owner lane moves to its next entry
+      if (lane == nb) { nv = bo_key_value(wk); ni = wi; }
+    }
+    if (nb == 0) return;
+    const bool probe = lane >= first_new && lane < nb;
+    const bool ex = probe && excluded(ni);
+    const bool ok = lane < nb && !ex;
+    wave_rank_insert(lv, li, nv, ni, ok, q, rbuf);
+    if (nb < q || __ballot(ex) == 0ull) return;  // the batch ended at the bound, or nothing was excluded
+  }
+}
+
+// The nw wave lists in wl[w q .. w q + q) (LDS, flat, sorted) merged into dst[0..q) (empty slots
+// -inf / -1): groups of 4 lists (4 q <= 64 contiguous entries, one per lane) ranked by one wave
+// each, level by level (the next level's lists again flat at wl[g q]).  Every thread of the
+// workgroup calls it.
+__device__ __forceinline__ void block_lists_merge(TopEntry* wl, int nw, int q, TopEntry* dst) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (nw == 1) {
+    __syncthreads();
+    if (threadIdx.x < q) dst[threadIdx.x] = wl[threadIdx.x];
+    return;
+  }
+  for (; nw > 1; nw = (nw + 3) / 4) {
+    __syncthreads();
+    const int groups = (nw + 3) / 4;
+    TopEntry e = {-__builtin_inf(), -1};
+    int rank = 64;
+    bool mine = false;
+    if (wave < groups) {
+      const int l0 = 4 * wave, nl = nw - l0 < 4 ? nw - l0 : 4, n = nl * q;
+      const TopEntry* g = wl + l0 * q;
+      mine = lane < n;
+      if (mine) e = g[lane];
+      const unsigned long long ke = bo_order_key(e.v, e.i);
+      rank = 0;
+      for (int t = 0; t < n; ++t) {
+        const TopEntry o = g[t];
+        rank += kbefore(bo_order_key(o.v, o.i), o.i, ke, e.i) ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    if (wave < groups) {
+      // valid entries have distinct indices (distinct ranks); empty slots fill the rest
+      const int nvalid = __popcll(__ballot(mine && e.i >= 0));
+      TopEntry* out = nw <= 4 ? dst : wl + wave * q;
+      if (mine && e.i >= 0 && rank < q) out[rank] = e;
+      if (lane >= nvalid && lane < q) out[lane] = TopEntry{-__builtin_inf(), -1};
+    }
+  }
+}
+
+// One span of the workgroup (16 waves): round 1, the bound, the rest (see above).  Every thread
+// of the workgroup calls it.
+// NW waves per workgroup (<= 16); SORTED: the lanes' entries arrive sorted (the merge's lists).
+template <int U, int NW, bool SORTED, class EX>
+__device__ __forceinline__ void block_span_select(LaneRun<U>& r, double& lv, long long& li, int q,
+                                                  TopEntry* rbuf, TopEntry* wmax, const EX& excluded) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if constexpr (!SORTED) r.sort();
+  r.h = 0;
+  // round 1: the wave's best non-excluded element (probed by lane 0)
+  unsigned long long wk;
+  long long wi;
+  for (;;) {
+    unsigned long long hk;
+    long long hi;
+    r.head(hk, hi);
+    wave_argbest(hk, hi, wk, wi);
+    if (wk == 0ull) break;
+    if (hi == wi) ++r.h;
+    const bool ex = __ballot(lane == 0 && excluded(wi)) != 0ull;
+    if (!ex) break;
+  }
+  if (lane == 0) { wmax[wave].v = bo_key_value(wk); wmax[wave].i = wk ? wi : -1; }
+  __syncthreads();
+  // B: the q-th best of the NW wave bests (lanes 0..NW-1 rank them); empty when fewer than q
+  unsigned long long bk = 0ull;
+  long long bi = -1;
+  {
+    const TopEntry me = lane < NW ? wmax[lane] : TopEntry{-__builtin_inf(), -1};
+    const unsigned long long mk = bo_order_key(me.v, me.i);
+    int rank = 0;
+#pragma unroll
+    for (int t = 0; t < NW; ++t) {
+      const TopEntry o = wmax[t];
+      rank += kbefore(bo_order_key(o.v, o.i), o.i, mk, me.i) ? 1 : 0;
+    }
+    const unsigned long long m = __ballot(lane < NW && me.i >= 0 && rank == q - 1);
+    if (m) {
+      const int s = __builtin_ctzll(m);
+      bk = bo_readlane_u(mk, s);
+      bi = bo_readlane_i(me.i, s);
+    }
+  }
+  __syncthreads();                               // wmax is rewritten by the next span
+  if (wk == 0ull || kbefore(bk, bi, wk, wi)) return;     // this wave's best is worse than B
+  // the wave's best is in; then up to q - 1 more strictly better than B
+  wave_extract<U>(r, bk, bi, lv, li, q, rbuf, excluded, wk, wi);
+}
+
+// Diagnostic build (BO_BUILD_VARIANT=DEF_SEL_TIMING): phase stamps of workgroups 0 and the last
+// (wave 0, real-time clock, 10 ns ticks) printed at the end of select_small_kernel.
+#ifdef BO_SEL_TIMING
+#include <stdio.h>
+#define SEL_STAMP(n) _t[n] = wall_clock64()
+#else
+#define SEL_STAMP(n) ((void)0)
+#endif
+
+template <int M, int U>
+__global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lkeys[];   // [lds_slots], then idx
+  __shared__ TopEntry rbuf[16][64];
+  __shared__ TopEntry wl[16 * 16];
+  __shared__ TopEntry wmax[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = a.topq;
+  const unsigned long long* hk = a.hkeys;
+  const int* hi = a.hidx;
+  unsigned int hm = a.hmask;
+  // workgroup spans of 16 x 64 U consecutive elements; load u of lane l of wave w reads
+  // element span + 64 (U w + u) + l
+  const long long wspan = 64LL * U;
+  const long long b_first = (long long)blockIdx.x * 16 * wspan;
+  const long long b_stride = (long long)gridDim.x * 16 * wspan;
+#ifdef BO_SEL_TIMING
+  long long _t[5];
+#endif
+  SEL_STAMP(0);
+  LaneRun<U> run;
+  auto load_span = [&](long long s0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long j = s0 + wave * wspan + 64 * u + lane;
+      const bool in = j < a.n_cand;
+      double v;
+      if constexpr (M == 0) {
+        v = in ? __builtin_nontemporal_load(a.acq + j) : 0.0;
+      } else {
+        double p[M];
+        bool nan = false;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
+          nan = nan || (p[k] != p[k]);
+        }
+        double hv = 0.0;
+        const double* b = h.boxes;
+        for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
+          double w = 1.0;
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            const double hi2 = p[k] < b[M + k] ? p[k] : b[M + k];
+            w *= fmax(hi2 - b[k], 0.0);
+          }
+          hv += w;
+        }
+        v = nan ? __builtin_nan("") : hv;
+        if (in) h.acq_out[j] = v;
+      }
+      run.i[u] = in ? a.cand_offset + j : -1;
+      run.k[u] = in ? bo_order_key(v, 0) : 0ull;
+    }
+  };
+  // the first span's loads go out before the hash build (they need no table)
+  if (b_first < a.n_cand) load_span(b_first);
+  if (a.lds_slots > 0) {
+    int* lidx = (int*)(lkeys + a.lds_slots);
+    for (int t = tid; t < a.lds_slots; t += blockDim.x) lkeys[t] = 0ull;
+    __syncthreads();
+    for (int e = tid; e < a.n_excl; e += blockDim.x) {
+      const unsigned long long key = bo_point_key(a.excl + (long long)e * a.dim, a.dim);
+      if (key != 0ull) bo_hash_insert(lkeys, lidx, (unsigned int)a.lds_slots - 1, key, e);
+    }
+    if (!BO_IN(a.n_excl, a.lds_slots / 2 + 1, "LDS hash load")) return;
+    __syncthreads();
+    hk = lkeys;
+    hi = lidx;
+    hm = (unsigned int)a.lds_slots - 1;
+  }
+  SEL_STAMP(1);
+  const SelExcl ex{&a, hk, hi, hm};
+  double lv = -__builtin_inf();
+  long long li = -1;
+  for (long long s0 = b_first; s0 < a.n_cand; s0 += b_stride) {     // workgroup-uniform
+    if (s0 != b_first) load_span(s0);
+#ifdef BO_SEL_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    SEL_STAMP(2);
+    block_span_select<U, 16, false>(run, lv, li, q, rbuf[wave], wmax, ex);
+  }
+  SEL_STAMP(3);
+  if (lane < q) { wl[wave * q + lane].v = lv; wl[wave * q + lane].i = li; }
+  block_lists_merge(wl, 16, q, a.partial + (size_t)blockIdx.x * q);
+#ifdef BO_SEL_TIMING
+  SEL_STAMP(4);
+  if ((blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && (threadIdx.x == 0 || threadIdx.x == 64 * 15))
+    printf("sel block %d wave %d: hash %lld loads %lld span %lld merge %lld ticks (x10 ns)\n", (int)blockIdx.x,
+           (int)(threadIdx.x >> 6), _t[1] - _t[0], _t[2] - _t[1], _t[3] - _t[2], _t[4] - _t[3]);
+#endif
+}
+
+// Final merge of n_lists sorted top-q lists ([n_lists][q], q <= U <= 16): one workgroup of 4
+// waves; a lane holds one list (sorted already), spans of 256 lists.
+template <int U>
+__global__ __launch_bounds__(256) void select_merge_kernel(const TopEntry* __restrict__ L, long long n_lists,
+                                                           int q, double* __restrict__ out_v,
+                                                           long long* __restrict__ out_i) {
+  __shared__ TopEntry rbuf[4][64];
+  __shared__ TopEntry wl[4 * 16];
+  __shared__ TopEntry wmax[4];
+  __shared__ TopEntry res[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double lv = -__builtin_inf();
+  long long li = -1;
+  const NoExcl ex;
+  LaneRun<U> run;
+  for (long long l0 = 0; l0 < n_lists; l0 += 256) {               // workgroup-uniform
+    const long long l = l0 + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const TopEntry e = (l < n_lists && u < q) ? L[l * q + u] : TopEntry{-__builtin_inf(), -1};
+      run.i[u] = e.i;
+      run.k[u] = e.i >= 0 ? bo_order_key(e.v, 0) : 0ull;
+    }
+    block_span_select<U, 4, true>(run, lv, li, q, rbuf[wave], wmax, ex);
+  }
+  if (lane < q) { wl[wave * q + lane].v = lv; wl[wave * q + lane].i = li; }
+  block_lists_merge(wl, 4, q, res);
+  __syncthreads();
+  if (threadIdx.x < q) {
+    const TopEntry e = res[threadIdx.x];
+    out_v[threadIdx.x] = e.i >= 0 ? e.v : -__builtin_inf();
+    out_i[threadIdx.x] = e.i;
+  }
+}
+
 template <int M, int U>
 __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lkeys[];   // [lds_slots], then idx
@@ -397,6 +771,24 @@ template <int M>
 int launch_select_stream(const SelArgs& a, const HviIn& h, int blocks, hipStream_t s) {
   const size_t lds = (size_t)a.lds_slots * 12;
   hipLaunchKernelGGL((select_stream_kernel<M, M == 0 ? 8 : 4>), dim3(blocks), dim3(256), lds, s, a, h);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+// elements per lane and span of select_small_kernel
+constexpr int kSmallU0 = 4;       // stored acquisition array: 4 loads of 8 B per lane, 16 waves per CU
+constexpr int kSmallUM = 4;       // exact HVI from the UCB arrays
+#ifdef BO_ABL_OLDSELECT
+constexpr int kSmallQ = 0;        // A/B: every q through select_stream_kernel + bo_topq_merge_kernel
+#else
+constexpr int kSmallQ = 4;        // q up to this: select_small_kernel + select_merge_kernel (faster at
+                                  // q <= 4; at q = 16 the event kernel: C3 44 vs 80 us, C5 79 vs 151 us)
+#endif
+
+template <int M>
+int launch_select_small(const SelArgs& a, const HviIn& h, int blocks, hipStream_t s) {
+  const size_t lds = (size_t)a.lds_slots * 12;
+  hipLaunchKernelGGL((select_small_kernel<M, M == 0 ? kSmallU0 : kSmallUM>), dim3(blocks), dim3(1024), lds, s, a, h);
   BO_CHECK_HIP(hipGetLastError());
   return BO_OK;
 }
@@ -603,6 +995,32 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
       a.hmask = slots - 1;
     }
   }
+  HviIn hz;
+  memset(&hz, 0, sizeof(hz));
+  const HviIn& hv = h ? *h : hz;
+  int st;
+  if (topq <= kSmallQ) {
+    // one span (16 waves x 64 U elements) per workgroup, one workgroup per CU; [blocks][q] lists
+    const long long per_block = 16LL * 64 * (m == 0 ? kSmallU0 : kSmallUM);
+    long long blocks = (n_cand + per_block - 1) / per_block;
+    const int max_blocks = cus_count() < 1024 ? cus_count() : 1024;
+    if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks < 1) blocks = 1;
+    switch (m) {
+      case 0: st = launch_select_small<0>(a, hv, (int)blocks, s); break;
+      case 1: st = launch_select_small<1>(a, hv, (int)blocks, s); break;
+      case 2: st = launch_select_small<2>(a, hv, (int)blocks, s); break;
+      case 3: st = launch_select_small<3>(a, hv, (int)blocks, s); break;
+      case 4: st = launch_select_small<4>(a, hv, (int)blocks, s); break;
+      default: return BO_ERR_UNSUPPORTED;
+    }
+    if (st != BO_OK) return st;
+    static_assert(kSmallQ <= 4, "select_merge_kernel<4> holds q <= 4 entries per list");
+    hipLaunchKernelGGL(select_merge_kernel<4>, dim3(1), dim3(256), 0, s, (const TopEntry*)ws, blocks,
+                       topq, top_val, (long long*)top_idx);
+    BO_CHECK_HIP(hipGetLastError());
+    return BO_OK;
+  }
   // U = 8 elements per thread and step (M == 0): one workgroup per 2048 elements, at most 4 per
   // CU (16 waves; the whole C3 array in flight at once); [blocks * 4][q] lists for the merge
   const long long per_block = 256LL * (m == 0 ? 8 : 4);
@@ -610,10 +1028,6 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   const int max_blocks = 4 * cus_count() < 1024 ? 4 * cus_count() : 1024;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
-  HviIn hz;
-  memset(&hz, 0, sizeof(hz));
-  const HviIn& hv = h ? *h : hz;
-  int st;
   switch (m) {
     case 0: st = launch_select_stream<0>(a, hv, (int)blocks, s); break;
     case 1: st = launch_select_stream<1>(a, hv, (int)blocks, s); break;

@@ -26,6 +26,9 @@ CASES = {  # name: (grid side0, side1, n evaluated, q)
     "C3q16": (1024, 1024, 512, 16),
     "C3q48": (1024, 1024, 512, 48),
     "C3noex": (1024, 1024, 0, 3),
+    "C3q1": (1024, 1024, 512, 1),
+    "C3q1noex": (1024, 1024, 0, 1),
+    "C3q16noex": (1024, 1024, 0, 16),
     "C5": (2048, 2048, 2048, 16),
 }
 
