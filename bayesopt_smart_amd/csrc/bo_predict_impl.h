@@ -221,7 +221,13 @@ __device__ __forceinline__ void mfma_fence(d4& x, d4& y) {
 #define BO_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | 0x70 | 0xF00)
 
 __device__ __forceinline__ d2 wload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+#ifdef BO_ABL_NOWLOAD
+  // ablation: no W traffic, operands from integer register moves (garbage values; timing only)
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(d2, (i4){voff, soff & 0x3FF, soff, 0x3C000000});
+#else
   return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+#endif
 }
 
 template <int PF>
@@ -272,7 +278,8 @@ struct EpChain<N, N> {
 };
 
 // K* values K*[f][j] = pv exp(-0.5 |x_f - c_j|^2 / ls^2) (numba_kernels.py:436-442) of lane j.
-//   SEP (integer 'ij' grid): rv[f] * T[rb[f] - jl] (row factor times the last-axis table);
+//   SEP (integer 'ij' grid): rv[f] * T[rb[f] - jl] (row factor times the last-axis table; rb
+//   and jl are kept as byte offsets and tbj = T - jl, so the address is ONE add per value);
 //   otherwise the exponent in base 2 with pv folded in, t = nl2 |x_f - c|^2 + log2 pv
 //   (nl2 = nhl log2 e), then exp2_tab.  Coordinates are CENTRED on z = training row 0 (xs holds
 //   x_f - z, c is c - z): distances are translation invariant, and f64 differences of centred
@@ -283,13 +290,14 @@ template <int DIM, bool SEP>
 struct KRows {
   double nl2, lpv;
   const double* rv;   // SEP: [n_pad] pv * R(f) (0 for padded rows)
-  const int* rb;      // SEP: [n_pad] table index base (x_f,last - lo_last) + S - 1; jl = col0 + lane
+  const int* rb;      // SEP: [n_pad] table index base ((x_f,last - lo_last) + S - 1) x 8 bytes
   const double* tb;   // SEP: objective's table T; otherwise the 2^(j/256) table
+  const char* tbj;    // SEP: T - jl (bytes), jl = col0 + lane: T[index] = *(tbj + rb[f])
   const double* xs;   // !SEP: training rows [n_pad][DIM] (padded rows at 1e200)
   double c[DIM];      // !SEP: this lane's candidate
   int jl;
   __device__ __forceinline__ double at(int f) const {
-    if (SEP) return rv[f] * tb[rb[f] - jl];
+    if (SEP) return rv[f] * *(const double*)(tbj + rb[f]);
     return exp2_tab(__builtin_fma(sqdist<DIM>(xs, f, c), nl2, lpv), tb);
   }
   // the 8 values of 32-row chunk `ch` this lane feeds to the MFMAs: rows 32 ch + 4 s + g
@@ -303,22 +311,23 @@ struct KRows {
 // pairs of the chunk's first E-pair (sched barriers pin them), so that every LDS round trip
 // of the generation (SEP: row factor + table index, then the table value; the alpha values
 // of the mean) completes under MFMAs instead of stalling the wave before the chunk:
-//   s0: rv[f], rb[f], alpha[f] loads     s1: table loads T[rb - jl] into Bn     s2: Bn *= rv.
+//   s0: rv[f], rb[f] (next chunk), alpha[f] (this chunk) loads   s1: table loads T[rb - jl] into
+//   Bn   s2: Bn *= rv.
 // The exp path (!SEP) is VALU work that serialises with f64 MFMAs anyway: all of it in s2.
-// The alpha values A of the next chunk are consumed (mu += A . Bn) right after s2, within the
-// same chunk, so that they need no second register set.
+// The mean takes the chunk being consumed (mu += A . B, every chunk once per group; the groups
+// after the first add to a copy that is dropped): no per-value select for the regenerated last
+// chunk or the later groups (every VALU instruction of this loop costs MFMA time).
 template <int DIM, bool SEP>
 struct KGen {
   using KR = KRows<DIM, SEP>;
   double rv[8];
   int rb[8];
-  __device__ __forceinline__ void s0(const KR& K, const double* al, bool mu_on, int ch,
-                                     int g, double (&A)[8]) {
+  __device__ __forceinline__ void s0(const KR& K, const double* al, int cha, int ch, int g,
+                                     double (&A)[8]) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
+      A[s] = al[32 * cha + 4 * s + g];
       const int f = 32 * ch + 4 * s + g;
-      const double a = al[f];
-      A[s] = mu_on ? a : 0.0;
       if (SEP) { rv[s] = K.rv[f]; rb[s] = K.rb[f]; }
     }
   }
@@ -336,7 +345,7 @@ struct KGen {
   __device__ __forceinline__ void s1(const KR& K, double (&B)[8]) {
     if (SEP) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) B[s] = K.tb[rb[s] - K.jl];
+      for (int s = 0; s < 8; ++s) B[s] = *(const double*)(K.tbj + rb[s]);
     }
   }
   __device__ __forceinline__ void s2(const KR& K, int ch, int g, double (&B)[8]) {
@@ -449,7 +458,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       }
       for (int o = o_lo; o < o_hi; ++o)
         rv[(size_t)(o - o_lo) * a.n_pad + f] = f < a.n_train ? a.pv[o] * exp(sqs * a.nhl[o]) : 0.0;
-      rb[f] = b;
+      rb[f] = b * 8;
       on[f] = onrow;
       const int col = b - (a.sep_S - 1);
       if (a.rw_cache && onrow && col >= 0 && col < a.sep_S) atomicOr(bm + (col >> 5), 1u << (col & 31));
@@ -489,6 +498,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       K.nl2 = a.nhl[o] * 1.4426950408889634;
       K.lpv = log2(a.pv[o]);
       K.jl = SEP ? col0 + jl : jl;   // T index = rb[f] - (col0 + jl) = x_f,last - c_last + S - 1
+      K.tbj = (const char*)K.tb - (size_t)K.jl * 8;
 #pragma unroll
       for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
       const double* al = alpha + (size_t)o * a.n_pad;
@@ -499,7 +509,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       d2 wa[PF], wb[PF];
       prime_ring(wr, voff, base, wa, wb);
       int pos = 0;
-      double mpart = 0.0, qpart = 0.0;
+      double mpart = 0.0, qpart = 0.0, msave = 0.0;
       d4 acc[MAXEP][2];
       // E-pairs in groups of kCMaxEp (the accumulators one wave holds: 512 rows); a group
       // streams the chunks that touch it (c >= its first E-pair when upper, all otherwise) and
@@ -517,9 +527,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #endif
         // one chunk: MFMAs from register set B while the next chunk's K* is generated into Bn
         // in three stages inside E-pair 0's MFMA stream (the sets alternate: no register
-        // copies between the chunks), then mu += alpha . Bn.  Branch-free: the last chunk
-        // regenerates itself (chn clamped; its alpha values zeroed) and groups after the first
-        // add 0 x alpha to mu.
+        // copies between the chunks), and mu += alpha . B.  Branch-free: the last chunk
+        // regenerates itself (chn clamped) and the groups after the first accumulate a mean
+        // that is dropped (msave).
         KGen<DIM, SEP> gen;
         auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8]) {
           double An[8];
@@ -535,13 +545,16 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             constexpr int e = decltype(e_c)::value;
             // explicit / Sobol candidates: keep the workgroup's 4 waves on the same E-pair block
             // (they stream identical W data, so 3 of 4 L2 requests become L1 hits).  W beyond
-            // an XCD's 4 MB L2 (C4: 12.6 MB, C5: 50 MB) otherwise comes from MALL once per
-            // wave: C5-f64 1124 -> 869 ms, C4 118.8 -> 116.8 ms (same box).  The SEP path is
-            // left unsynchronised (lockstep measured 4 % slower at C3, 7 % at C2: its W fits L2).
+            // the L2s (C5: 50 MB) otherwise comes from MALL once per wave: C5-f64 1124 -> 869 ms
+            // (round 2, same box).  The SEP path is left unsynchronised (lockstep measured 4 %
+            // slower at C3, 7 % at C2: its W fits L2).
             // (a barrier every 2nd or 4th body measured the same at C4 / C5-f64)
-            if constexpr (!SEP) __builtin_amdgcn_s_barrier();
+            // only in the GROWS kernels (N beyond the LDS rows: W of tens of MB, C5-f64); at
+            // C4 (12.6 MB, L2 hit rate 95 %) the barrier cost 1.7 % (110.1 vs 108.3 ms), and a
+            // runtime switch around it cost 1 % more in both settings
+            if constexpr (!SEP && GROWS) __builtin_amdgcn_s_barrier();
             if constexpr (e == 0) {
-              gen.s0(K, al, e0 == 0 && chn != ch, chn, g, An);
+              gen.s0(K, al, ch, chn, g, An);
               __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
@@ -568,7 +581,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
                 } else if (pp == 3) {
                   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                  for (int s = 0; s < 8; ++s) mpart = __builtin_fma(An[s], Bn[s], mpart);
+                  for (int s = 0; s < 8; ++s) mpart = __builtin_fma(An[s], B[s], mpart);
                   __builtin_amdgcn_sched_barrier(0);
                 }
               }
@@ -596,10 +609,6 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         const int c0 = upper ? nch - 1 : 0;
         double BX[8], BY[8];
         K.chunk(c0, g, BX);
-        if (e0 == 0) {
-#pragma unroll
-          for (int s = 0; s < 8; ++s) mpart = __builtin_fma(al[32 * c0 + 4 * s + g], BX[s], mpart);
-        }
         int ch = c0;
         if (upper) {
           for (; ch - 1 >= e0; ch -= 2) {
@@ -640,7 +649,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             }
           }
         }
+        if (e0 == 0) msave = mpart;             // the mean is group 0's (every chunk once)
       }
+      mpart = msave;
       if (upper) qpart *= 2.0;
       qpart += __shfl_xor(qpart, 16, 64);
       qpart += __shfl_xor(qpart, 32, 64);
@@ -690,7 +701,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           // columns; OR over the wave, bit jl is this lane's candidate
           unsigned int xmask = 0;
           for (int f = lane; f < a.n_train; f += 64) {
-            const int dx = rb[f] - (a.sep_S - 1) - col0;
+            const int dx = (rb[f] >> 3) - (a.sep_S - 1) - col0;
             if (on[f] && dx >= 0 && dx < 16) xmask |= 1u << dx;
           }
           unsigned int m = xmask;
@@ -894,7 +905,7 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
 #pragma unroll
       for (int q = 0; q < 16; ++q) w[q] = wload32(wr, voff, base + q * 1024);
       int pos = 0;
-      float mpart = 0.0f, qpart = 0.0f;
+      float mpart = 0.0f, qpart = 0.0f, msave = 0.0f;
       f4 acc[kC32MaxEp][4];
       for (int e0 = 0; e0 < nch; e0 += kC32MaxEp) {
         const int eN = nch - e0 < kC32MaxEp ? nch - e0 : kC32MaxEp;
@@ -902,7 +913,6 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
         for (int e = 0; e < kC32MaxEp; ++e)
 #pragma unroll
           for (int b = 0; b < 4; ++b) acc[e][b] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
-        const bool mu_on = e0 == 0;
         auto chunk_step = [&](int ch, const float (&B)[16], float (&Bn)[16]) {
           const int chn = ch > e0 ? ch - 1 : ch;
           const int n_here = ch - e0 + 1 < eN ? ch - e0 + 1 : eN;
@@ -917,7 +927,7 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
 #pragma unroll
               for (int s = 0; s < 16; ++s) {
                 const float av = alo[64 * ch + 16 * (s >> 2) + 4 * g + (s & 3)];
-                mpart = __builtin_fmaf(mu_on ? av : 0.0f, B[s], mpart);
+                mpart = __builtin_fmaf(av, B[s], mpart);   // group 0's is kept (msave)
               }
               chunk(chn, Bn);
             }
@@ -950,7 +960,9 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
           chunk_step(ch - 1, BY, BX);
         }
         if (ch >= e0) chunk_step(ch, BX, BY);
+        if (e0 == 0) msave = mpart;
       }
+      mpart = msave;
       qpart += __shfl_xor(qpart, 16, 64);
       qpart += __shfl_xor(qpart, 32, 64);
       mpart += __shfl_xor(mpart, 16, 64);
