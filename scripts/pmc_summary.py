@@ -49,6 +49,9 @@ def main(src, dst, workload="C3", alg_bytes=40 * 1048576, kernel_label="cm_predi
                             "algorithmic = outputs written (+ explicit coordinates read)"})
     if "SQ_INSTS_MFMA" in mean and "SQ_INSTS_VALU" in mean:
         out["valu_per_mfma"] = mean["SQ_INSTS_VALU"] / max(mean["SQ_INSTS_MFMA"], 1.0)
+        # SQ_INSTS_VALU counts the MFMAs too (C4: 2.7 per MFMA against ~1.7 other VALU per MFMA
+        # counted in the ISA); the other vector ALU instructions per MFMA:
+        out["non_mfma_valu_per_mfma"] = out["valu_per_mfma"] - 1.0
     if "SQ_WAIT_INST_ANY" in mean and "SQ_BUSY_CYCLES" in mean:
         out["wait_inst_any_per_busy_cycle"] = mean["SQ_WAIT_INST_ANY"] / max(mean["SQ_BUSY_CYCLES"], 1.0)
     with open(dst, "w") as fh:
