@@ -542,10 +542,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             // (round 2, same box).  The SEP path is left unsynchronised (lockstep measured 4 %
             // slower at C3, 7 % at C2: its W fits L2).
             // (a barrier every 2nd or 4th body measured the same at C4 / C5-f64)
-            // only in the GROWS kernels (N beyond the LDS rows: W of tens of MB, C5-f64); at
-            // C4 (12.6 MB, L2 hit rate 95 %) the barrier cost 1.7 % (110.1 vs 108.3 ms), and a
-            // runtime switch around it cost 1 % more in both settings
-            if constexpr (!SEP && GROWS) __builtin_amdgcn_s_barrier();
+            // Round 3: without it C4 ran 1.7 % faster (108.3 vs 110.1 ms) but fetched 84 GB
+            // per launch from beyond the L2 instead of 22 GB, and C5-f64 (W 50 MB) ran 982 vs
+            // 822 ms at 4.7 TB of fetches; a runtime switch around the barrier cost 1 % in both
+            // settings.  Kept for every explicit / Sobol kernel.
+            if constexpr (!SEP) __builtin_amdgcn_s_barrier();
             if constexpr (e == 0) {
               gen.s0(K, al, ch, chn, g, An);
               __builtin_amdgcn_sched_barrier(0);

@@ -115,6 +115,7 @@ struct SelArgs {
   unsigned int hmask;
   TopEntry* partial;
   long long partial_cap;    // entries of `partial` (the debug build checks every write)
+  int idx32;                // grid: every global index below 2^31 (32-bit decode)
   SobolArgs sob;            // kind BO_CAND_SOBOL
 };
 
@@ -134,7 +135,19 @@ __device__ __forceinline__ bool cand_excluded(const SelArgs& a, long long j,
                                               const unsigned long long* hk, const int* hi,
                                               unsigned int hm) {
   double c[BO_MAX_DIM];
-  if (a.kind == BO_CAND_GRID) {          // all coordinates from one chain of divisions
+  if (a.kind == BO_CAND_GRID && a.idx32) {   // 32-bit divisions (the 64-bit ones are ~10x longer)
+    unsigned int gi = (unsigned int)(a.cand_offset + j);
+#pragma unroll
+    for (int k = BO_MAX_DIM - 1; k >= 0; --k) {
+      c[k] = 0.0;
+      if (k < a.dim) {
+        const unsigned int n = (unsigned int)a.grid_shape[k];
+        const unsigned int q = gi / n;
+        c[k] = (double)(a.grid_lo[k] + (long long)(gi - q * n));
+        gi = q;
+      }
+    }
+  } else if (a.kind == BO_CAND_GRID) {   // all coordinates from one chain of divisions
     long long gi = a.cand_offset + j;
 #pragma unroll
     for (int k = BO_MAX_DIM - 1; k >= 0; --k) {
@@ -966,12 +979,16 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
     a.cand = nullptr;
   }
   for (int k = 0; k < BO_MAX_DIM; ++k) a.grid_shape[k] = 1;
-  if (kind == BO_CAND_GRID)
+  if (kind == BO_CAND_GRID) {
     for (int k = 0; k < dim; ++k) {
       if (grid_shape[k] <= 0) return BO_ERR_ARG;
       a.grid_lo[k] = grid_lo[k];
       a.grid_shape[k] = grid_shape[k];
     }
+    a.idx32 = cand_offset >= 0 && cand_offset + n_cand < (1LL << 31) ? 1 : 0;
+    for (int k = 0; k < dim; ++k)
+      if (grid_shape[k] >= (1LL << 31)) a.idx32 = 0;
+  }
   a.excl = excl;
   a.partial = (TopEntry*)ws;
   a.partial_cap = (long long)(sel_lists_bytes(topq) / sizeof(TopEntry));

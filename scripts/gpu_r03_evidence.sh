@@ -53,6 +53,7 @@ timeout -k 10 400 python -u bench.py --acq hvi > $E/hvi_bench.jsonl 2> $E/hvi_be
 for c in C3 C4 C5; do
   timeout -k 10 400 python -u bench.py --fit --config $c >> $E/fit.jsonl 2>> $E/fit.err || { echo "fit $c failed"; exit 1; }
 done
+timeout -k 10 300 python -u scripts/select_ubench.py > $E/select_ubench.jsonl 2>&1 || { echo "select ubench failed"; exit 1; }
 echo benches ok
 for c in C3 C2; do
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$E/prof_$c" -o run -- \
