@@ -409,7 +409,7 @@ __device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g
     for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
     if (lane == 0) {
       part[(long long)o * part_len(g) + k] = v;
-      if (bad) atomicOr(status + o, 1);
+      if (bad) status[o] = 1;                  // MLL: one flag, plain store (pinned host memory)
     }
   }
   if (sb == g.nbt && lane == NB) {                               // the bottom row z = L^-1 (y - pm)
@@ -829,8 +829,15 @@ int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const dou
   hipStream_t s = (hipStream_t)stream;
   const Geo g = make_geo((int)n, n_obj, false);
   double* A = (double*)ws;
-  double* part = (double*)((char*)ws + geo_bytes(g));
+  // the per-step partials and the status flags go straight to pinned host memory (plain device
+  // stores; visible after the stream synchronisation): no status memset and no read-back copy
+  // per call -- two launches and their boundaries less per Powell evaluation
+  const size_t bytes = (size_t)n_obj * part_len(g) * sizeof(double) + sizeof(int) * n_obj;
+  double* h = (double*)pinned(bytes);
+  if (!h) return BO_ERR_HIP;
+  double* part = h;
   int* status = (int*)(part + (size_t)n_obj * part_len(g));
+  for (int o = 0; o < n_obj; ++o) status[o] = 0;
   FitParams p;
   memset(&p, 0, sizeof(p));
   for (int o = 0; o < n_obj; ++o) {
@@ -839,13 +846,8 @@ int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const dou
     p.ls2[o] = ls[o] * ls[o];
   }
   p.jitter = BO_CHOLESKY_JITTER;               // numba_kernels.py:211-214
-  BO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * n_obj, s));
   int st = fit_factor(A, g, km, ld, x, dim, y, ld_y, p, part, status, s);
   if (st != BO_OK) return st;
-  const size_t bytes = (size_t)n_obj * part_len(g) * sizeof(double) + sizeof(int) * n_obj;
-  double* h = (double*)pinned(bytes);
-  if (!h) return BO_ERR_HIP;
-  BO_CHECK_HIP(hipMemcpyAsync(h, part, bytes, hipMemcpyDeviceToHost, s));
   BO_CHECK_HIP(hipStreamSynchronize(s));
   const int* hstat = (const int*)(h + (size_t)n_obj * part_len(g));
   for (int o = 0; o < n_obj; ++o)
