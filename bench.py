@@ -641,8 +641,9 @@ def main():
             res["front_hypervolume"] = {"value": hv_front, "reference_point": ref_pt.tolist(),
                                         "method": f"bo_box_volume_sum over this rank's share of the "
                                                   f"{n_boxes[0]} boxes + all_reduce(SUM) over {world} rank(s)"}
-            res["hvi_select"] = {"kernels": f"select_stream_kernel<{n_obj}, 4> "
-                                            "+ bo_topq_merge_kernel (exact HVI + top-q, one pass)",
+            res["hvi_select"] = {"kernels": (f"select_small_kernel<{n_obj}, 4> + select_merge_kernel<4>" if q <= 4 else
+                                             f"select_stream_kernel<{n_obj}, 4> + bo_topq_merge_kernel")
+                                            + " (exact HVI + top-q, one pass)",
                                  "ms": hms, "n_boxes": n_boxes[0], "front_points": int(front_y.shape[0]),
                                  "bytes_per_candidate": 8 * n_obj + 8,
                                  "achieved_GBps": hb / (hms * 1e-3) / 1e9,
@@ -721,7 +722,8 @@ def standalone_select(lib, bo, acq, cands, offset, n, xd, q, dev, fused_sel, rep
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    return {"kernels": "select_stream_kernel<0, 8> + bo_topq_merge_kernel (HIP-graph replay)",
+    return {"kernels": ("select_small_kernel<0, 4> + select_merge_kernel<4>" if q <= 4 else
+                        "select_stream_kernel<0, 8> + bo_topq_merge_kernel") + " (HIP-graph replay)",
             "ms": ms, "bytes": 8 * n, "achieved_GBps": 8 * n / (ms * 1e-3) / 1e9,
             "hbm_frac": 8 * n / (ms * 1e-3) / 1e9 / 8000.0,
             "matches_fused_selection": bool(np.array_equal(got[got >= 0], np.asarray(fused_sel)))}
