@@ -311,17 +311,19 @@ __device__ void pack32_range(long long t0, long long stride, f4* __restrict__ ou
 
 
 // ---------------------------------------------------------------------------------------
-// Per-call preparation, ONE launch (blocks by role):
-//   [0, pack_blocks)               W packed into the kernel's MFMA stream (pack_cm_range /
-//                                  pack_range / pack32_range);
-//   [.., + alpha_blocks)           alpha[o][f] = sum_e K^-1[o][f][e] (y[e][o] - pm[o])
-//                                  (numba_kernels.py:477-483), one wave per row, e ascending
-//                                  per lane then a shuffle tree;
-//   last block                     training rows: xpad (original; padded rows 1e200 so their
+// Per-call preparation, ONE launch (blocks by role; the two single-block roles, serial chains of
+// dependent memory round trips, come first so that they are dispatched before the bulk):
+//   block 0                        training rows: xpad (original; padded rows 1e200 so their
 //                                  K* is exactly 0) and xc = x - x_0 (centred); the
 //                                  separable-grid precondition flag (every training point's last
 //                                  coordinate an integer on the grid's last axis); the
-//                                  evaluated points padded to [n_excl][DIM].
+//                                  evaluated points padded to [n_excl][DIM];
+//   block 1                        the hash set of the exclusion rows (zeroed, then filled);
+//   [2, 2 + alpha_blocks)          alpha[o][f] = sum_e K^-1[o][f][e] (y[e][o] - pm[o])
+//                                  (numba_kernels.py:477-483), one wave per row, e ascending
+//                                  per lane then a shuffle tree;
+//   [.., + pack_blocks)            W packed into the kernel's MFMA stream (pack_cm_range /
+//                                  pack_range / pack32_range).
 // ---------------------------------------------------------------------------------------
 struct PrepArgs {
   int pack_mode;                         // 0 chunk-major (cm), 1 panels (kmem), 2 f32 (cm32)
@@ -355,14 +357,61 @@ struct PrepArgs {
 __global__ __launch_bounds__(256) void predict_prep_kernel(const PrepArgs p) {
   const int tid = threadIdx.x;
   int b = blockIdx.x;
-  if (b < p.pack_blocks) {
-    const long long t0 = (long long)b * 256 + tid, stride = (long long)p.pack_blocks * 256;
-    if (p.pack_mode == 0) pack_cm_range(t0, stride, (d2*)p.wpack, p.kinv, p.ld_k, p.upper, p.n, p.n_pad, p.n_obj);
-    else if (p.pack_mode == 1) pack_range(t0, stride, (d2*)p.wpack, p.kinv, p.ld_k, p.n, p.n_pad, p.ns, p.n_obj);
-    else pack32_range(t0, stride, (f4*)p.wpack, p.kinv, p.ld_k, p.n, p.n_pad, p.n_obj);
+  if (b == 0) {
+    if (!p.rows) return;
+    int sep_bad = 0;
+    for (int f = tid; f < p.n_pad; f += 256) {
+      for (int k = 0; k < p.DIM; ++k) {
+        const bool real = f < p.n && k < p.dim;
+        const double v = f < p.n ? (real ? p.x[(long long)f * p.dim + k] : 0.0) : 1e200;
+        p.xpad[(long long)f * p.DIM + k] = v;
+        p.xc[(long long)f * p.DIM + k] = f < p.n ? v - (k < p.dim ? p.x[k] : 0.0) : 1e200;
+      }
+      if (f < p.n && p.sep_flag) {
+        const double v = p.x[(long long)f * p.dim + p.dim - 1];
+        const bool ok = v == __builtin_rint(v) && v >= (double)p.sep_lo && v <= (double)(p.sep_lo + p.sep_S - 1);
+        sep_bad |= !ok;
+      }
+    }
+    const int any_bad = __syncthreads_or(sep_bad);
+    if (tid == 0 && p.sep_flag) *p.sep_flag = any_bad ? 1 : 0;
+    for (int t = tid; t < p.n_excl * p.DIM; t += 256) {
+      const int r = t / p.DIM, k = t - r * p.DIM;
+      p.excl[t] = k < p.dim ? p.excl_in[(long long)r * p.dim + k] : 0.0;
+    }
     return;
   }
-  b -= p.pack_blocks;
+  if (b == 1) {
+    if (p.n_hash <= 0) return;
+    // keys over the DIM-padded coordinates (zeros past dim), read from the inputs; the first
+    // 4 x 256 rows' keys are computed before the table is zeroed, so that their loads overlap it
+    const double* src = p.excl_in ? p.excl_in : p.x;
+    constexpr int KP = 4;
+    unsigned long long kp[KP];
+#pragma unroll
+    for (int u = 0; u < KP; ++u) {
+      const int e = tid + 256 * u;
+      kp[u] = 0ull;
+      if (e < p.n_hash) {
+        double c[BO_MAX_DIM];
+        for (int k = 0; k < p.DIM; ++k) c[k] = k < p.dim ? src[(long long)e * p.dim + k] : 0.0;
+        kp[u] = bo_point_key(c, p.DIM);
+      }
+    }
+    for (unsigned int t = tid; t < p.hslots; t += 256) p.hkeys[t] = 0ull;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < KP; ++u)
+      if (kp[u] != 0ull) bo_hash_insert(p.hkeys, p.hidx, p.hslots - 1, kp[u], tid + 256 * u);
+    for (int e = tid + 256 * KP; e < p.n_hash; e += 256) {
+      double c[BO_MAX_DIM];
+      for (int k = 0; k < p.DIM; ++k) c[k] = k < p.dim ? src[(long long)e * p.dim + k] : 0.0;
+      const unsigned long long key = bo_point_key(c, p.DIM);
+      if (key != 0ull) bo_hash_insert(p.hkeys, p.hidx, p.hslots - 1, key, e);
+    }
+    return;
+  }
+  b -= 2;
   const int lane = tid & 63, wave = tid >> 6;
   if (b < p.alpha_blocks) {
     const long long row_id = (long long)b * 4 + wave;
@@ -379,39 +428,11 @@ __global__ __launch_bounds__(256) void predict_prep_kernel(const PrepArgs p) {
     if (lane == 0) p.alpha[row_id] = s;
     return;
   }
-  if (!p.rows) return;
-  int sep_bad = 0;
-  for (int f = tid; f < p.n_pad; f += 256) {
-    for (int k = 0; k < p.DIM; ++k) {
-      const bool real = f < p.n && k < p.dim;
-      const double v = f < p.n ? (real ? p.x[(long long)f * p.dim + k] : 0.0) : 1e200;
-      p.xpad[(long long)f * p.DIM + k] = v;
-      p.xc[(long long)f * p.DIM + k] = f < p.n ? v - (k < p.dim ? p.x[k] : 0.0) : 1e200;
-    }
-    if (f < p.n && p.sep_flag) {
-      const double v = p.x[(long long)f * p.dim + p.dim - 1];
-      const bool ok = v == __builtin_rint(v) && v >= (double)p.sep_lo && v <= (double)(p.sep_lo + p.sep_S - 1);
-      sep_bad |= !ok;
-    }
-  }
-  const int any_bad = __syncthreads_or(sep_bad);
-  if (tid == 0 && p.sep_flag) *p.sep_flag = any_bad ? 1 : 0;
-  for (int t = tid; t < p.n_excl * p.DIM; t += 256) {
-    const int r = t / p.DIM, k = t - r * p.DIM;
-    p.excl[t] = k < p.dim ? p.excl_in[(long long)r * p.dim + k] : 0.0;
-  }
-  if (p.n_hash > 0) {
-    for (unsigned int t = tid; t < p.hslots; t += 256) p.hkeys[t] = 0ull;
-    __syncthreads();
-    // keys over the DIM-padded coordinates (zeros past dim), read from the inputs
-    const double* src = p.excl_in ? p.excl_in : p.x;
-    for (int e = tid; e < p.n_hash; e += 256) {
-      double c[BO_MAX_DIM];
-      for (int k = 0; k < p.DIM; ++k) c[k] = k < p.dim ? src[(long long)e * p.dim + k] : 0.0;
-      const unsigned long long key = bo_point_key(c, p.DIM);
-      if (key != 0ull) bo_hash_insert(p.hkeys, p.hidx, p.hslots - 1, key, e);
-    }
-  }
+  b -= p.alpha_blocks;
+  const long long t0 = (long long)b * 256 + tid, stride = (long long)p.pack_blocks * 256;
+  if (p.pack_mode == 0) pack_cm_range(t0, stride, (d2*)p.wpack, p.kinv, p.ld_k, p.upper, p.n, p.n_pad, p.n_obj);
+  else if (p.pack_mode == 1) pack_range(t0, stride, (d2*)p.wpack, p.kinv, p.ld_k, p.n, p.n_pad, p.ns, p.n_obj);
+  else pack32_range(t0, stride, (f4*)p.wpack, p.kinv, p.ld_k, p.n, p.n_pad, p.n_obj);
 }
 
 __global__ void selftest_mfma32_kernel(const float* a, const float* b, float* d) {
@@ -737,7 +758,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     pa.hidx = (int*)fa.hidx;
     pa.hslots = pl.hash_slots;
     pa.n_hash = (kmem || d->topq == 0) ? 0 : pl.n_excl;
-    hipLaunchKernelGGL(predict_prep_kernel, dim3((unsigned)(pa.pack_blocks + pa.alpha_blocks + 1)), dim3(256),
+    hipLaunchKernelGGL(predict_prep_kernel, dim3((unsigned)(2 + pa.alpha_blocks + pa.pack_blocks)), dim3(256),
                        0, s, pa);
     BO_CHECK_HIP(hipGetLastError());
   }
