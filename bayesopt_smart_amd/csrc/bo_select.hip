@@ -513,37 +513,58 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
   SEL_STAMP(0);
   LaneRun<U> run;
   auto load_span = [&](long long s0) {
+    if constexpr (M == 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long j = s0 + wave * wspan + 64 * u + lane;
-      const bool in = j < a.n_cand;
-      double v;
-      if constexpr (M == 0) {
-        v = in ? __builtin_nontemporal_load(a.acq + j) : 0.0;
-      } else {
-        double p[M];
-        bool nan = false;
+      for (int u = 0; u < U; ++u) {
+        const long long j = s0 + wave * wspan + 64 * u + lane;
+        const bool in = j < a.n_cand;
+        const double v = in ? __builtin_nontemporal_load(a.acq + j) : 0.0;
+        run.i[u] = in ? a.cand_offset + j : -1;
+        run.k[u] = in ? bo_order_key(v, 0) : 0ull;
+      }
+    } else {
+      // the U elements' UCB loads first, then the boxes outer: one (wave-uniform) load of a box
+      // serves the lane's U elements; per element the sum over boxes and the product over
+      // objectives run in the standalone scan's order (bit-identical acq)
+      double p[U][M], hv[U];
+      bool nan[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long j = s0 + wave * wspan + 64 * u + lane;
+        const bool in = j < a.n_cand;
+        nan[u] = false;
+        hv[u] = 0.0;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
-          p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
-          nan = nan || (p[k] != p[k]);
+          p[u][k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
+          nan[u] = nan[u] || (p[u][k] != p[u][k]);
         }
-        double hv = 0.0;
-        const double* b = h.boxes;
-        for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
+      }
+      const double* b = h.boxes;
+      for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
+        double lo[M], up[M];
+#pragma unroll
+        for (int k = 0; k < M; ++k) { lo[k] = b[k]; up[k] = b[M + k]; }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
           double w = 1.0;
 #pragma unroll
           for (int k = 0; k < M; ++k) {
-            const double hi2 = p[k] < b[M + k] ? p[k] : b[M + k];
-            w *= fmax(hi2 - b[k], 0.0);
+            const double hi2 = p[u][k] < up[k] ? p[u][k] : up[k];
+            w *= fmax(hi2 - lo[k], 0.0);
           }
-          hv += w;
+          hv[u] += w;
         }
-        v = nan ? __builtin_nan("") : hv;
-        if (in) h.acq_out[j] = v;
       }
-      run.i[u] = in ? a.cand_offset + j : -1;
-      run.k[u] = in ? bo_order_key(v, 0) : 0ull;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long j = s0 + wave * wspan + 64 * u + lane;
+        const bool in = j < a.n_cand;
+        const double v = nan[u] ? __builtin_nan("") : hv[u];
+        if (in) h.acq_out[j] = v;
+        run.i[u] = in ? a.cand_offset + j : -1;
+        run.k[u] = in ? bo_order_key(v, 0) : 0ull;
+      }
     }
   };
   // the first span's loads go out before the hash build (they need no table)

@@ -416,6 +416,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # BO_BENCH_BACKEND=gloo: a functional rehearsal of the multi-rank step with several ranks on
+    # one device (not a measurement); the product launch is one rank per GPU over RCCL
+    backend = os.environ.get("BO_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.fit or args.fit_demo:
@@ -425,7 +430,10 @@ def main():
               flush=True)
         return
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import bayesopt_smart_amd as bo
     from bayesopt_smart_amd.distributed import shard_range
@@ -528,8 +536,13 @@ def main():
         else:
             run()
         if world > 1:
-            dist.all_gather_into_tensor(gath, rec)
-            g = gath.view(world, 2 * q).cpu()
+            if backend == "nccl":
+                dist.all_gather_into_tensor(gath, rec)
+                g = gath.view(world, 2 * q).cpu()
+            else:
+                g = torch.empty(world * 2 * q, dtype=torch.float64)
+                dist.all_gather_into_tensor(g, rec.cpu())
+                g = g.view(world, 2 * q)
             return bo.merge_topq(g[:, :q].numpy(), g[:, q:].contiguous().view(torch.int64).numpy(), q)
         # one shard: the device list is already merged and in selection order
         if rec_np is not None:
@@ -572,7 +585,8 @@ def main():
         from bayesopt_smart_amd.distributed import front_hypervolume
         hv_front = front_hypervolume(front_y, ref_pt, device=dev)
     if world > 1:
-        tt = torch.tensor([t_step, kms.value / max(nl.value, 1)], dtype=torch.float64, device=dev)
+        tt = torch.tensor([t_step, kms.value / max(nl.value, 1)], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_step, k_ms = tt.tolist()
     else:
