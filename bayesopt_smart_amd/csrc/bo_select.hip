@@ -829,7 +829,7 @@ int launch_select_small(const SelArgs& a, const HviIn& h, int blocks, hipStream_
 
 // --------------------------------------------------------------------------- Pareto
 // mask[i] = 0 iff some row j (j != i) weakly dominates row i under maximisation:
-// y_j >= y_i in every objective and y_j > y_i in at least one (pareto.py:279-287 with
+// y_j >= y_i in every objective and y_j > y_i in at least one (pareto.py:35-41 with
 // y negated).  Comparisons only: bit-exact, NaN never dominates nor is dominated.
 // The reference's scan order (break on the first dominator, marks only rows it
 // reaches) yields exactly this set; see oracle/oracle_np.py:is_pareto_efficient.
