@@ -239,7 +239,13 @@ def cpu_baseline(x, y, pm, pv, ls, betas, kinv, points, label, q, max_cand=SIDE 
     t_med = float(np.median(times))
     done = sample
     if sample < max_cand and max_cand <= full_limit:     # untimed: the rest, for the parity fields
-        acq = np.concatenate([acq] + [run(lo, min(lo + chunk, max_cand)) for lo in range(sample, max_cand, chunk)])
+        parts, t_log = [acq], time.perf_counter()
+        for lo in range(sample, max_cand, chunk):
+            parts.append(run(lo, min(lo + chunk, max_cand)))
+            if time.perf_counter() - t_log > 30.0:      # progress of a long untimed scoring (C5 --cpu-full)
+                print(f"[bench] cpu reference: {lo + chunk} of {max_cand} candidates scored", file=sys.stderr, flush=True)
+                t_log = time.perf_counter()
+        acq = np.concatenate(parts)
         done = max_cand
     cpu_sel = cpu_ref.select(acq, points(0, done), x, q)
     res = {"value": sample / t_med, "unit": "candidate-points/sec", "cores": threads, "kind": "port",
