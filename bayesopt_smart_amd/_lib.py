@@ -22,8 +22,8 @@ MAX_TOPQ = 48
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_WORKSPACE, ERR_HIP, ERR_NOT_PD, ERR_SINGULAR = range(7)
 CAND_I64, CAND_F64, CAND_GRID, CAND_SOBOL = 0, 1, 2, 3
-ABI_VERSION = 2
-MODE_AUTO, MODE_DENSE, MODE_NO_SEPARABLE = 0, 1, 2
+ABI_VERSION = 3
+MODE_AUTO, MODE_DENSE, MODE_NO_SEPARABLE, MODE_FP32, MODE_F32_FLOOR = 0, 1, 2, 4, 8
 
 c_dbl_p = C.POINTER(C.c_double)
 c_vp = C.c_void_p
@@ -53,6 +53,17 @@ class PredictDesc(C.Structure):
         ("topq", C.c_int32), ("reserved1", C.c_int32),
         ("top_val", c_vp), ("top_idx", c_vp),
     ]
+
+
+class PowellResult(C.Structure):
+    """Mirror of bo_powell_result (include/bo_amd.h)."""
+
+    _fields_ = [("fun", C.c_double), ("nfev", C.c_int64), ("nit", C.c_int64),
+                ("device_calls", C.c_int64), ("warnflag", C.c_int32), ("reserved", C.c_int32)]
+
+
+# int (*)(const double* x, int32_t n, double* f, void* user)
+OBJECTIVE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_double), C.c_void_p)
 
 
 class SobolDesc(C.Structure):
@@ -96,7 +107,19 @@ _SIGS = {
     "bo_box_volume_sum": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_dbl_p, c_vp, c_vp]),
     "bo_invert_k": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, c_vp, C.c_size_t, c_vp]),
     "bo_invert_k_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
+    "bo_invert_k_jitter": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, C.c_double, c_vp,
+                                     C.c_size_t, c_vp]),
+    "bo_compute_mll_each_jitter": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,
+                                             C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, C.c_double,
+                                             c_vp, C.c_size_t, c_vp]),
+    "bo_powell_minimize": (C.c_int, [OBJECTIVE_FN, c_vp, c_dbl_p, C.c_int32, c_dbl_p, c_dbl_p, C.c_double,
+                                     C.c_double, C.c_int64, C.c_int64, c_dbl_p, C.POINTER(PowellResult)]),
+    "bo_optimize_hyperparams_mll": (C.c_int, [c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64, C.c_int32,
+                                              c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, C.c_double, C.c_double,
+                                              C.c_double, C.c_int64, C.c_double, c_vp, C.c_size_t, c_vp,
+                                              C.POINTER(PowellResult), c_dbl_p]),
     "bo_invert_k_path_counts": (C.c_int, [C.POINTER(C.c_int64)]),
+    "bo_fit_path_counts": (C.c_int, [C.POINTER(C.c_int64)]),
     "bo_compute_mll": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,
                                  C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, c_vp, C.c_size_t,
                                  c_vp]),
@@ -159,6 +182,13 @@ def invert_k_path_counts():
     arr = (C.c_int64 * 3)()
     check(load().bo_invert_k_path_counts(arr), "bo_invert_k_path_counts")
     return {"cholesky": arr[0], "lu": arr[1], "gauss_jordan": arr[2]}
+
+
+def fit_path_counts():
+    """{'persistent', 'launches', 'aborted'}: how the factorisations so far were scheduled."""
+    arr = (C.c_int64 * 3)()
+    check(load().bo_fit_path_counts(arr), "bo_fit_path_counts")
+    return {"persistent": arr[0], "launches": arr[1], "aborted": arr[2]}
 
 
 def dbl_array(values, n=None):

@@ -32,7 +32,7 @@ from . import kernels as K
 from .acquisition import hvi_select_indices, select_indices, update_hypervolume_improvement_exact
 from .config import (DEFAULT_BATCH_SIZE, DEFAULT_BETA, DEFAULT_INITIAL_SAMPLES,
                      DEFAULT_LENGTH_SCALE, DEFAULT_PRIOR_MEAN, DEFAULT_PRIOR_VARIANCE,
-                     NUMBA_FLOAT_TYPE)
+                     resolve_float_type)
 from .device import F64, require_device
 from .pareto import compute_pareto_front, print_pareto_analysis
 from .predict import CandidateSet, predict_acquire
@@ -83,15 +83,18 @@ def _world(group=None):
     return 0, 1
 
 
-def _broadcast_np(arr, group=None):
-    """Broadcast a float64 numpy array (or view) from rank 0 in place; a no-op on one rank.  The
-    collective's tensor lives where the backend needs it (HIP for RCCL, host for gloo)."""
+def _broadcast_np(arr, group=None, device=None):
+    """Broadcast a numpy array (or view) from rank 0 in place; a no-op on one rank.  The
+    collective's tensor lives where the backend needs it: on `device` (the backend's HIP device,
+    default the current one) for RCCL, on the host for gloo."""
     import torch.distributed as dist
     _, world = _world(group)
     if world == 1 or np.size(arr) == 0:
         return arr
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
-        else torch.device("cpu")
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
     t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float64), device=dev)
     dist.broadcast(t, 0, group=group)
     arr[...] = t.cpu().numpy().reshape(np.shape(arr))
@@ -110,11 +113,17 @@ class DeviceBackend:
 
     `state_arrays` gives the callbacks' mu / variance / acquisition arrays over the whole set:
     this rank's buffers, or the shards gathered (a collective: every rank's loop calls it at the
-    same point)."""
+    same point).
 
-    def __init__(self, cands, n_obj, total_samples, device=None, buffers=None, group=None):
+    float_type np.float32 (the reference's float32 branch, config.py:54-66): the fit runs COBYLA
+    with the float32 jitters (numba_kernels.py:290-302), invert_k adds 1e-3, and the predict runs
+    the f32 matrix-core kernel (mode "fp32") with the variance floor 1e-6."""
+
+    def __init__(self, cands, n_obj, total_samples, device=None, buffers=None, group=None, float_type=None):
         from .distributed import shard_range
         self.dev = require_device(device)
+        self.float_type = resolve_float_type(float_type)
+        self.mode = "fp32" if self.float_type == np.float32 else "auto"
         self.cands = cands
         self.group = group
         self.rank, self.world = _world(group)
@@ -128,12 +137,12 @@ class DeviceBackend:
         xd = torch.as_tensor(np.ascontiguousarray(x_vector[:n], dtype=np.float64), device=self.dev)
         yd = torch.as_tensor(np.ascontiguousarray(y_vector[:n], dtype=np.float64), device=self.dev)
         optimized = K.optimize_hyperparams_mll(xd, yd, self.bufs.kernel_matrices, prior_mean,
-                                               prior_variance, length_scales, n)
-        _broadcast_np(length_scales, self.group)
-        _broadcast_np(prior_variance, self.group)
+                                               prior_variance, length_scales, n, float_type=self.float_type)
+        _broadcast_np(length_scales, self.group, self.dev)
+        _broadcast_np(prior_variance, self.group, self.dev)
         t1 = time.perf_counter()
         K.update_k(self.bufs.kernel_matrices, xd, 0, n, prior_variance, length_scales)
-        kinv = K.invert_k(n, self.bufs.kernel_matrices)
+        kinv = K.invert_k(n, self.bufs.kernel_matrices, float_type=self.float_type)
         torch.cuda.synchronize(self.dev)
         return optimized, (xd, yd, kinv), t1
 
@@ -156,11 +165,12 @@ class DeviceBackend:
             from .distributed import sharded_predict_acquire
             _, (_, idx) = sharded_predict_acquire(xd, yd, kinv, self.cands, prior_mean, prior_variance,
                                                   length_scales, betas, batch_size, outputs=tuple(out),
-                                                  group=self.group, device=self.dev, out=out)
+                                                  group=self.group, device=self.dev, out=out, mode=self.mode,
+                                                  float_type=self.float_type)
             return np.asarray(idx, dtype=np.int64)
         predict_acquire(xd, yd, kinv, self.cands, prior_mean, prior_variance, length_scales, betas,
                         outputs=tuple(out), topq=0, offset=self.offset, count=self.count, out=out,
-                        device=self.dev)
+                        device=self.dev, mode=self.mode, float_type=self.float_type)
         if acquisition == "hvi" and batch_size <= _lib.MAX_TOPQ:
             # the exact HVI and its top-q with exclusion in one device pass over this shard, then
             # the fused path's exchange
@@ -198,7 +208,8 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
              prior_mean, prior_variance, reference_point, n_evaluations, total_samples,
              n_objectives, function, betas, length_scales, batch_size, bounds,
              callbacks: Optional[List[Callable]] = None, *,
-             acquisition: str = "sum_ucb", group=None, backend=None) -> Tuple[np.ndarray, np.ndarray, int]:
+             acquisition: str = "sum_ucb", group=None, backend=None,
+             float_type=None) -> Tuple[np.ndarray, np.ndarray, int]:
     """bayesian_optimization.py:51-247 with the reference's argument list.
 
     `kernel_matrices` and the posterior arrays may be HIP tensors (in place) or numpy arrays;
@@ -211,7 +222,12 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
     shard of the candidates (module docstring); the posterior arrays given here are then not
     filled (each rank holds its shard), the state dict's arrays are the gathered whole.  `group`
     selects the process group; `backend` replaces the device side (DeviceBackend's interface:
-    fit / select / state_arrays / cands / rank / world / bufs).
+    fit / select / state_arrays / cands / rank / world / bufs).  `float_type` np.float32 runs the
+    reference's float32 branch (DeviceBackend).
+
+    Callbacks with several ranks: the state arrays are the shards gathered, a collective; whether
+    to gather is decided once, collectively (any rank with callbacks), so that a callback
+    registered on rank 0 only keeps every rank's collectives matched.
     """
     del k_star, n_objectives, bounds  # unused, as in the reference (reference_point too, unless
     #                                   acquisition="hvi", the exact hypervolume improvement)
@@ -236,8 +252,15 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
         bufs.std_variance_objectives = dev_buf(std_variance_objectives, (n_obj, cnt))
         bufs.ucb = dev_buf(ucb, (n_obj, cnt))
         bufs.acquisition_values = dev_buf(acquisition_values, (cnt,))
-        backend = DeviceBackend(cands, n_obj, total_samples, dev, bufs, group)
+        backend = DeviceBackend(cands, n_obj, total_samples, dev, bufs, group, float_type=float_type)
     cands, rank, world = backend.cands, backend.rank, backend.world
+    gather = bool(callbacks)
+    if world > 1:                       # any rank with callbacks: every rank joins the gathers
+        import torch.distributed as dist
+        flag = torch.tensor([1.0 if callbacks else 0.0], dtype=torch.float64,
+                            device=backend.dev if dist.get_backend(backend.group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=backend.group)
+        gather = bool(flag.item())
 
     last_eval = 0
     for current_eval in range(n_evaluations, total_samples, batch_size):
@@ -255,11 +278,13 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
             if rank == 0:       # the user's objective, once per point (bayesian_optimization.py:213-216)
                 y_vector[current_eval + b_idx] = function(point)
         if world > 1:
-            _broadcast_np(y_vector[current_eval:current_eval + len(x_next)], backend.group)
+            _broadcast_np(y_vector[current_eval:current_eval + len(x_next)], backend.group,
+                          getattr(backend, "dev", None))
         last_eval = current_eval
         t4 = time.perf_counter()
-        if callbacks:
+        if gather:
             arrs = backend.state_arrays()
+        if callbacks:
             state = LazyState({
                 "iteration": current_eval,
                 "n_evaluations": current_eval + batch_size,
@@ -315,62 +340,87 @@ class BayesianOptimization:
     """bayesian_optimization.py:250-488 — same constructor, kwargs and methods.
 
     Extra kwargs (not in the reference): ``input_space`` (explicit [M, d] candidates, e.g.
-    a Sobol set, instead of the integer grid), ``device``, ``acquisition`` ("sum_ucb", the
-    reference's default, or "hvi": exact hypervolume improvement of the UCB vectors over the
-    evaluated Pareto front), ``reference_point`` (the HVI reference point; the reference
-    fixes it at zeros and never uses it, bayesian_optimization.py:425) and ``group`` (the
-    torch.distributed process group of a multi-GPU run; default: the world when initialised).
-    With several ranks, each holds its shard of the posterior arrays, the initial design's
-    objective values are rank 0's (broadcast) and the loop runs as `optimize` describes.
+    a Sobol set, or a CandidateSet such as CandidateSet.sobol_set(...), instead of the integer
+    grid), ``device``, ``acquisition`` ("sum_ucb", the reference's default, or "hvi": exact
+    hypervolume improvement of the UCB vectors over the evaluated Pareto front),
+    ``reference_point`` (the HVI reference point; the reference fixes it at zeros and never uses
+    it, bayesian_optimization.py:425), ``group`` (the torch.distributed process group of a
+    multi-GPU run; default: the world when initialised), ``float_type`` (np.float64, the default
+    of config.NUMBA_FLOAT_TYPE, or np.float32: the reference's float32 branch -- config.py:54-66
+    jitters and variance floor, COBYLA for the fit, float32 host arrays -- with the predict on the
+    f32 matrix cores) and ``initial_points`` ([n0, d] points evaluated as the initial design
+    instead of the Latin hypercube).
+    With several ranks, each holds its shard of the posterior arrays, the initial design is drawn
+    and evaluated on rank 0 (every rank draws the same RNG numbers, so the RNG stays in step) and
+    broadcast, and the loop runs as `optimize` describes.
     """
 
     def __init__(self, function: Callable[[np.ndarray], np.ndarray], bounds: List[Tuple[int, int]],
                  n_objectives: int = 3, n_iterations: int = 10, **kwargs: Any):
         self.device = require_device(kwargs.get("device"))
         self.group = kwargs.get("group")
+        self.float_type = resolve_float_type(kwargs.get("float_type"))
+        ft = self.float_type
         self.function = function
         self.bounds = bounds
         self.n_objectives = n_objectives
         self.n_iterations = n_iterations
         cb = kwargs.get("callbacks", None)
         self.callbacks = [] if cb is None else (cb if isinstance(cb, list) else [cb])
-        self.prior_mean = np.array(kwargs.get("prior_mean", [DEFAULT_PRIOR_MEAN] * n_objectives),
-                                   dtype=NUMBA_FLOAT_TYPE)
+        self.prior_mean = np.array(kwargs.get("prior_mean", [DEFAULT_PRIOR_MEAN] * n_objectives), dtype=ft)
         self.prior_variance = np.array(kwargs.get("prior_variance", [DEFAULT_PRIOR_VARIANCE] * n_objectives),
-                                       dtype=NUMBA_FLOAT_TYPE)
-        self.length_scales = np.array(kwargs.get("length_scales", [DEFAULT_LENGTH_SCALE] * n_objectives),
-                                      dtype=NUMBA_FLOAT_TYPE)
-        self.betas = np.array(kwargs.get("betas", [DEFAULT_BETA] * n_objectives), dtype=NUMBA_FLOAT_TYPE)
+                                       dtype=ft)
+        self.length_scales = np.array(kwargs.get("length_scales", [DEFAULT_LENGTH_SCALE] * n_objectives), dtype=ft)
+        self.betas = np.array(kwargs.get("betas", [DEFAULT_BETA] * n_objectives), dtype=ft)
         self.batch_size = kwargs.get("batch_size", DEFAULT_BATCH_SIZE)
-        self.initial_samples = kwargs.get("initial_samples", DEFAULT_INITIAL_SAMPLES)
+        init_pts = kwargs.get("initial_points")
+        if init_pts is not None:
+            init_pts = np.asarray(init_pts)
+            if init_pts.ndim != 2 or init_pts.shape[1] != len(bounds):
+                raise ValueError("initial_points must be [n0, len(bounds)]")
+        self.initial_samples = init_pts.shape[0] if init_pts is not None else \
+            kwargs.get("initial_samples", DEFAULT_INITIAL_SAMPLES)
         self.dim = len(bounds)
         explicit = kwargs.get("input_space")
-        self.candidates = (CandidateSet.grid(bounds) if explicit is None
-                           else CandidateSet.explicit(explicit, self.device))
+        if explicit is None:
+            self.candidates = CandidateSet.grid(bounds)
+        elif isinstance(explicit, CandidateSet):
+            self.candidates = explicit
+        else:
+            self.candidates = CandidateSet.explicit(explicit, self.device)
         self._input_space = None
         self.total_samples = self.initial_samples + self.n_iterations * self.batch_size
         self.acquisition = kwargs.get("acquisition", "sum_ucb")
         if self.acquisition not in ("sum_ucb", "hvi"):
             raise ValueError(f"unknown acquisition {self.acquisition!r} (expected 'sum_ucb' or 'hvi')")
         _check_limits(n_objectives, self.dim, self.total_samples, self.batch_size, self.acquisition)
-        self.x_vector = np.zeros((self.total_samples, self.dim), dtype=NUMBA_FLOAT_TYPE)
-        self.y_vector = np.zeros((self.total_samples, n_objectives), dtype=NUMBA_FLOAT_TYPE)
+        self.x_vector = np.zeros((self.total_samples, self.dim), dtype=ft)
+        self.y_vector = np.zeros((self.total_samples, n_objectives), dtype=ft)
         self._backend = DeviceBackend(self.candidates, n_objectives, self.total_samples, self.device,
-                                      group=self.group)
+                                      group=self.group, float_type=ft)
         self._buffers = self._backend.bufs
         self.k_star = None   # never materialised (the reference allocates n_obj x T x M here)
-        self.n_evaluations = K.initialize_lhs_integer(self.x_vector, self.y_vector,
-                                                      np.array(self.bounds, dtype=np.int64),
-                                                      self.function, self.initial_samples)
-        # several ranks: rank 0's initial design is everyone's
-        _broadcast_np(self.x_vector[: self.n_evaluations], self.group)
-        _broadcast_np(self.y_vector[: self.n_evaluations], self.group)
+        rank, world = _world(self.group)
+        # the objective runs on rank 0 only; the other ranks draw the same LHS numbers (their RNG
+        # stays in step with rank 0's) and receive rank 0's design and values
+        fn = self.function if rank == 0 else (lambda _p: np.zeros(n_objectives))
+        if init_pts is not None:
+            for i in range(self.initial_samples):
+                self.x_vector[i] = init_pts[i]
+                self.y_vector[i] = fn(self.x_vector[i])
+            self.n_evaluations = self.initial_samples
+        else:
+            self.n_evaluations = K.initialize_lhs_integer(self.x_vector, self.y_vector,
+                                                          np.array(self.bounds, dtype=np.int64),
+                                                          fn, self.initial_samples)
+        _broadcast_np(self.x_vector[: self.n_evaluations], self.group, self.device)
+        _broadcast_np(self.y_vector[: self.n_evaluations], self.group, self.device)
         if np.all(self.prior_mean == DEFAULT_PRIOR_MEAN):
-            self.prior_mean = K.compute_prior_mean(self.y_vector, self.n_evaluations, n_objectives)
+            self.prior_mean = K.compute_prior_mean(self.y_vector, self.n_evaluations, n_objectives).astype(ft)
         if np.all(self.prior_variance == DEFAULT_PRIOR_VARIANCE):
-            self.prior_variance = K.compute_prior_variance(self.y_vector, self.n_evaluations, n_objectives)
-        self.reference_point = np.array(kwargs.get("reference_point", [0.0] * n_objectives),
-                                        dtype=NUMBA_FLOAT_TYPE)
+            self.prior_variance = K.compute_prior_variance(self.y_vector, self.n_evaluations,
+                                                           n_objectives).astype(ft)
+        self.reference_point = np.array(kwargs.get("reference_point", [0.0] * n_objectives), dtype=ft)
 
     # the reference's preallocated arrays, materialised on the host on demand
     @property
@@ -403,7 +453,8 @@ class BayesianOptimization:
             total_samples=self.total_samples, n_objectives=self.n_objectives, function=self.function,
             betas=self.betas, length_scales=self.length_scales, batch_size=self.batch_size,
             bounds=self.bounds, callbacks=self.callbacks if self.callbacks else None,
-            acquisition=self.acquisition, group=self.group, backend=self._backend)
+            acquisition=self.acquisition, group=self.group, backend=self._backend,
+            float_type=self.float_type)
 
     def pareto_analysis(self) -> np.ndarray:
         """bayesian_optimization.py:465-488."""

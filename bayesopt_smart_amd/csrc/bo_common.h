@@ -35,6 +35,7 @@ __device__ __forceinline__ bool bo_bound(bool ok, const char* what, long long v,
 
 // MIN_VARIANCE / KERNEL_JITTER / CHOLESKY_JITTER: bayesopt/config.py:57-66 (fp64 branch).
 #define BO_MIN_VARIANCE 1e-10
+#define BO_MIN_VARIANCE_F32 1e-6    // the float32 branch's floor (config.py:57-61), BO_PREDICT_F32_FLOOR
 #define BO_KERNEL_JITTER 1e-6
 #define BO_CHOLESKY_JITTER 1e-8
 
@@ -442,8 +443,8 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
 // invert_k's blocked LU path (bo_lu.hip), called by bo_invert_k (bo_fit.hip) per objective
 size_t bo_lu_workspace_size(int64_t n);
 int bo_lu_max_n();
-int bo_lu_inverse(double* out, const double* km, int64_t ld, int64_t n, void* ws, size_t ws_bytes,
-                  hipStream_t s);
+int bo_lu_inverse(double* out, const double* km, int64_t ld, int64_t n, double jitter, void* ws,
+                  size_t ws_bytes, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------
 // Sobol candidates (BO_CAND_SOBOL): direction numbers (host) and one coordinate (device).

@@ -41,6 +41,7 @@
 #include "bo_common.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -145,11 +146,21 @@ __global__ __launch_bounds__(256) void fit_init_kernel(double* __restrict__ A, G
                                                        const double* __restrict__ x, int dim,
                                                        const double* __restrict__ y, long long ld_y,
                                                        FitParams p, double* __restrict__ part,
-                                                       int* __restrict__ status, int tiles_per_obj) {
+                                                       int* __restrict__ status, int tiles_per_obj,
+                                                       int* __restrict__ flags, long long n_flags) {
   __shared__ double tile[NB][NB + 1];
   __shared__ double red[256];
   const int tid = threadIdx.x;
   const long long np_ = (long long)g.nbt * NB;
+  const int work_blocks = g.n_obj * tiles_per_obj + (g.ident ? 0 : g.n_obj);
+  if ((int)blockIdx.x >= work_blocks) {
+    // the persistent factorisation's flag words (dequeue counter, panel flags, tile versions):
+    // zeroed here, one launch before the kernel that polls them
+    for (long long i = (long long)(blockIdx.x - work_blocks) * 256 + tid; i < n_flags;
+         i += (long long)(gridDim.x - work_blocks) * 256)
+      flags[i] = 0;
+    return;
+  }
   if ((int)blockIdx.x >= g.n_obj * tiles_per_obj) {
     // var(y - pm) of one objective (two passes, as np.std)
     const int o = blockIdx.x - g.n_obj * tiles_per_obj;
@@ -366,14 +377,14 @@ __device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g
       rsqrt_sqrt(piv, rs, d);
       a[j] = lane == j ? d : a[j] * rs;                         // lanes > j: L_ij; lanes < j: unused
       dj = lane == j ? d : dj;
-      // column j is final: store it now (diagonal rows >= j by workgroup 0, every slab row), so
-      // that the stores drain under the rest of the factorisation
+      // column j is final: store it now (the slab rows; the diagonal tile's L is read by no later
+      // step and the step's other panel workgroups read that tile's input), so that the stores
+      // drain under the rest of the factorisation
       // (a buffer store: the lane's row offset in one VGPR, the column offset in an SGPR -- plain
       // stores kept 32 64-bit addresses live and spilled)
       // branch-free: the lanes that must not store get an offset past the resource (dropped)
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, a[j]), colr,
-                                            (lane >= NB || (w_slab == 0 && lane >= j)) ? row_off : 0x40000000,
-                                            j * col_bytes, 0);
+                                            lane >= NB ? row_off : 0x40000000, j * col_bytes, 0);
 #pragma unroll
       for (int t = j + 1; t < j0 + FG; ++t) a[t] = __builtin_fma(-a[j], bo_readlane_d(a[j], t), a[t]);
     }
@@ -643,6 +654,433 @@ __global__ void gather_cols_kernel(double* __restrict__ out, const double* __res
   out[t] = B[(long long)i * n + perm[j]];
 }
 
+// ------------------------------------------------------------- persistent factorisation
+// The same factorisation as one launch (after fit_init_kernel): the launch-per-step schedule's
+// work units become TASKS of one queue that every workgroup of a persistent grid dequeues in
+// order (one returning atomic add per task), each task waiting only on tasks before it in the
+// queue (a dependency flag per panel and a version counter per tile): the kernel boundary per
+// 32-column step (~3.7 us at N = 512, profiles/r03_fit_stamps_a.txt) becomes a flag hand-off,
+// and the panel of step k+1 starts while the bulk of step k's trailing update still runs.
+//
+// Tasks of block k (the old launch k), in queue order:
+//   A_{k-1}[k+1]   step k-1 applied to column block k+1's tiles (what the panel of step k+1 needs;
+//                  4 tiles per task, one per wave)
+//   P(k, w)        the panel of step k for slab k+1+w (applies step k-1 to its rows of column
+//                  block k, factors the diagonal tile redundantly and solves the slab)
+//   A_{k-1}[rest]  step k-1 applied to column blocks >= k+2 (and to the inverse's C block)
+// Every dependency points backwards (P(k) needs P(k-1) and A_{k-2}[k]; A_s needs P(s) and the
+// tile's previous version), so any number of resident workgroups makes progress: the queue order
+// is a topological order and a workgroup takes its next task only after finishing the current.
+//
+// Hand-off (MI355X guide, Guideline 16, R1 with sc1 loads): every store of A is an sc1 store, every
+// load of A an sc1 load (L1 bypassed: no acquire needed); each storing wave drains vmcnt(0), the
+// workgroup meets at a barrier, then one lane stores the flag (relaxed, agent scope).  Waits are
+// bounded: a wave that spins past the bound (or sees another's abort) sets the abort word and
+// the task is skipped; the host then reruns the call on the launch-per-step path.
+constexpr int PMAX_STEPS = 128;
+
+struct PPlan {
+  int steps, total;
+  int blk[PMAX_STEPS + 1];                   // first task of block k
+};
+
+// flag words (fit_init_kernel zeroes them): [0] dequeue counter, [1] abort; per objective from
+// word 16: pflag [nbt][nbt] (P(k) of slab k+1+w done), tver [RB][nbt] (L-part tile versions:
+// steps applied), tverC [nbt][nbt] (the inverse's C tiles)
+__host__ __device__ inline int p_rb(const Geo& g) { return g.ident ? 2 * g.nbt : g.nbt + 1; }
+__host__ __device__ inline long long p_per_obj(const Geo& g) {
+  return 2ll * g.nbt * g.nbt + (long long)p_rb(g) * g.nbt;
+}
+__host__ __device__ inline long long p_flag_words(const Geo& g) { return 16 + g.n_obj * p_per_obj(g); }
+__device__ __forceinline__ int* pf_panel(int* f, const Geo& g, int o, int k, int w) {
+  return f + 16 + o * p_per_obj(g) + (long long)k * g.nbt + w;
+}
+__device__ __forceinline__ int* pf_tver(int* f, const Geo& g, int o, int rb, int cb) {
+  return f + 16 + o * p_per_obj(g) + (long long)g.nbt * g.nbt + (long long)rb * g.nbt + cb;
+}
+__device__ __forceinline__ int* pf_tverc(int* f, const Geo& g, int o, int b, int cp) {
+  return f + 16 + o * p_per_obj(g) + (long long)g.nbt * g.nbt + (long long)p_rb(g) * g.nbt + (long long)b * g.nbt + cp;
+}
+
+__device__ __forceinline__ int ld_flag(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The calling wave waits until *fp >= want on every active lane (one flag per lane, all loads in
+// flight at once).  false on abort: the spin bound (~1 s) passed here or another wave gave up.
+__device__ bool wave_wait(const int* fp, int want, bool active, int* abort_w) {
+  for (unsigned spins = 0;; ++spins) {
+    const bool ok = !active || ld_flag(fp) >= want;
+    if (__ballot(!ok) == 0ull) return true;
+    if ((spins & 63u) == 63u) {
+      if (ld_flag(abort_w) != 0) return false;
+      if (spins > (1u << 20)) {
+        if ((threadIdx.x & 63) == 0) st_flag(abort_w, 1);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// rows of L-part row block rb start receiving updates at step s0 (the inverse's bottom block b
+// is structurally zero in column blocks < b)
+__device__ __forceinline__ int p_s0(const Geo& g, int rb) { return (g.ident && rb >= g.nbt) ? rb - g.nbt : 0; }
+
+__device__ __forceinline__ int p_n1(const Geo& g, int k) {      // tiles per objective of A_{k-1}[k+1]
+  if (k < 1 || k + 1 >= g.nbt) return 0;
+  return g.ident ? g.nbt - 1 : g.nbt - k;
+}
+__device__ __forceinline__ int p_npanel(const Geo& g, int k) { return k < g.nbt ? (g.ident ? g.nbt : g.nbt - k) : 0; }
+__device__ __forceinline__ void p_n2(const Geo& g, int k, long long& TL2, long long& TC) {
+  TL2 = 0;
+  TC = 0;
+  if (k < 1) return;
+  const long long m2 = g.nbt - k - 2, base = g.ident ? k + 1 : 2;
+  TL2 = m2 > 0 ? m2 * base + m2 * (m2 - 1) / 2 : 0;
+  TC = g.ident ? (long long)k * (k + 1) / 2 : 0;
+}
+
+struct PTile {
+  int o, rb, cb;            // L part: row / column block; C part: b / cp
+  bool cpart, first;
+};
+
+// One 32 x 32 tile of step s's trailing update on one wave (the update role's body with sc1
+// loads and stores).  Returns after the wave's stores are issued.
+__device__ __forceinline__ void p_tile_update(double* __restrict__ A, const Geo& g, int s, const PTile& t) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
+  const long long np_ = (long long)g.nbt * NB;
+  long long row0, col0;
+  if (t.cpart) {
+    row0 = np_ + (long long)t.rb * NB;
+    col0 = np_ + (long long)t.cb * NB;
+  } else {
+    row0 = (long long)t.rb * NB;
+    col0 = (long long)t.cb * NB;
+  }
+  double* Ao = A + (long long)t.o * g.ostride;
+  const long long Na = g.Na;
+  const double* Lp = Ao + (long long)s * NB * Na;
+  double cv[2][2][4];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        cv[tb][rb][i] = t.first ? 0.0 : ld_sc1(Ao + (col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li);
+  double av[2][8], bv[2][8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      av[h][ks] = ld_sc1(Lp + (4 * ks + lg) * Na + col0 + 16 * h + li);
+      bv[h][ks] = ld_sc1(Lp + (4 * ks + lg) * Na + row0 + 16 * h + li);
+    }
+  d4 acc[2][2];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = mfma64(av[tb][ks], bv[rb][ks], acc[tb][rb]);
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        st_sc1(Ao + (col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li, cv[tb][rb][i] - acc[tb][rb][i]);
+}
+
+// The panel of step k for slab sb = k + 1 + w of objective o, on the whole workgroup: step k-1's
+// update of the diagonal tile and the slab (MFMA, 4 waves x 16 rows), then the 32-column
+// factorisation with the columns split over the waves: wave g owns columns 8g..8g+7 for all 64
+// rows (lane = row: 0..31 the diagonal tile, 32..63 the slab).  Wave g factors its 8 columns
+// (in-wave pivot chain: readlane -> rsqrt -> scale -> readlane -> fma), publishes them in LDS,
+// and every later wave applies their rank-8 update to its own columns: the critical path holds 4
+// groups of 8 pivots plus 3 rank-8 updates, where one wave used to do all 32 columns' updates.
+__device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, int o, int k, int w,
+                                        double* __restrict__ part, int* __restrict__ status,
+                                        double* Cs, double* colb, double* red) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const long long Na = g.Na;
+  const long long cK = (long long)k * NB;
+  const int sb = k + 1 + w;
+  const int lr0 = 16 * wave;
+  const long long grow0 = wave < 2 ? cK + lr0 : (long long)sb * NB + (lr0 - 32);
+  const int ntb = wave == 0 ? 1 : 2;
+  double av_a[2][4];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 16 * tb + lg + 4 * i;
+      av_a[tb][i] = (tb < ntb && !(wave < 2 && lr0 + li < t)) ? ld_sc1(Ao + (cK + t) * Na + grow0 + li) : 0.0;
+    }
+  d4 acc[2];
+  acc[0] = (d4){0.0, 0.0, 0.0, 0.0};
+  acc[1] = acc[0];
+  if (k > 0) {
+    const double* Lp = Ao + (cK - NB) * Na;
+    double av[2][8], bv[8];
+    const bool zero_rows = g.ident && wave >= 2 && sb == g.nbt + k;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) bv[ks] = zero_rows ? 0.0 : ld_sc1(Lp + (4 * ks + lg) * Na + grow0 + li);
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        av[tb][ks] = tb < ntb ? ld_sc1(Lp + (4 * ks + lg) * Na + cK + 16 * tb + li) : 0.0;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      acc[0] = mfma64(av[0][ks], bv[ks], acc[0]);
+      if (ntb > 1) acc[1] = mfma64(av[1][ks], bv[ks], acc[1]);
+    }
+  }
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 16 * tb + lg + 4 * i;
+      Cs[(lr0 + li) * CS + t] = av_a[tb][i] - acc[tb][i];
+    }
+  __syncthreads();
+  // wave g: columns 8g .. 8g + 7 of every row
+  const int c0 = 8 * wave;
+  double a[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) a[c] = Cs[lane * CS + c0 + c];
+  const int col_bytes = (int)(Na * 8);
+  const __amdgpu_buffer_rsrc_t colr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Ao + cK * Na), (short)0, NB * col_bytes, 0x00020000);
+  const long long row_l = lane < NB ? cK + lane : (long long)sb * NB + lane - NB;
+  const int row_off = (int)(row_l * 8);
+  double dj = 1.0;
+  bool bad = false;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (wave == p) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int J = 8 * p + j;                                 // == c0 + j (wave == p)
+        const double piv = bo_readlane_d(a[j], J);
+        bad = bad || !(piv > 0.0);                               // potrf: a_jj <= 0 or NaN
+        double rs, d;
+        rsqrt_sqrt(piv, rs, d);
+        a[j] = lane == J ? d : a[j] * rs;
+        dj = lane == J ? d : dj;
+        // column J is final: the slab rows store it at once, write-through (sc1: the hand-off
+        // to other CUs).  The diagonal tile's L is read by no later task (the panels of step k+1
+        // and the trailing updates read only rows below it), and the other panels of this step
+        // still read that tile's input values: it is not stored.
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, a[j]), colr,
+                                              lane >= NB ? row_off : 0x40000000, J * col_bytes, 16);
+#pragma unroll
+        for (int t = j + 1; t < 8; ++t) a[t] = __builtin_fma(-a[j], bo_readlane_d(a[j], 8 * p + t), a[t]);
+      }
+      if (p < 3) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) colb[(p * 64 + lane) * 8 + c] = a[c];
+      }
+    }
+    if (p < 3) {
+      __syncthreads();
+      if (wave > p) {                                            // rank-8 update from group p
+        const double* L = colb + p * 64 * 8;
+        double lr[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) lr[c] = L[lane * 8 + c];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          double s0 = a[t];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) s0 = __builtin_fma(-lr[c], L[(c0 + t) * 8 + c], s0);
+          a[t] = s0;
+        }
+      }
+    }
+  }
+  // per-wave partials (own columns), combined through LDS
+  double ldp = (lane >= c0 && lane < c0 + 8 && cK + lane < g.n) ? log(dj) : 0.0;
+  double zp = 0.0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) zp = __builtin_fma(a[c], a[c], zp);
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) ldp += __shfl_xor(ldp, m, 64);
+  const double z_lane = __shfl(zp, NB, 64);                     // slab row 0 = the bottom row (MLL)
+  if (lane == 0) {
+    red[wave] = ldp;
+    red[4 + wave] = z_lane;
+    red[8 + wave] = bad ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const bool any_bad = red[8] + red[9] + red[10] + red[11] != 0.0;
+    if (g.ident) {
+      if (w == 0 && any_bad) atomicOr(status + o, 1);
+    } else {
+      if (w == 0) {
+        part[(long long)o * part_len(g) + k] = ((red[0] + red[1]) + red[2]) + red[3];
+        if (any_bad) status[o] = 1;
+      }
+      if (sb == g.nbt) part[(long long)o * part_len(g) + g.nbt + k] = ((red[4] + red[5]) + red[6]) + red[7];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict__ A, Geo g, PPlan pl,
+                                                             int* __restrict__ flags, double* __restrict__ part,
+                                                             int* __restrict__ status, int* __restrict__ habort) {
+  __shared__ double Cs[2 * NB * CS];
+  __shared__ double colb[3 * 64 * 8];
+  __shared__ double red[16];
+  __shared__ int s_task;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int* abort_w = flags + 1;
+  while (true) {
+    if (tid == 0) s_task = atomicAdd(flags, 1);                  // dequeue (returning atomic)
+    __syncthreads();
+    const int t = s_task;
+    __syncthreads();                                             // s_task is rewritten next round
+    if (t >= pl.total) return;
+    // block k: blk[k] <= t < blk[k + 1]
+    int lo = 0, hi = pl.steps - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pl.blk[mid] <= t) lo = mid;
+      else hi = mid - 1;
+    }
+    const int k = lo;
+    int r = t - pl.blk[k];
+    const int n1 = p_n1(g, k);
+    const int T1 = (g.n_obj * n1 + 3) / 4;
+    const int nP = g.n_obj * p_npanel(g, k);
+    if (r >= T1 && r < T1 + nP) {
+      // ---- panel P(k, w)
+      const int np = p_npanel(g, k);
+      const int o = (r - T1) / np, w = (r - T1) % np;
+      const int sb = k + 1 + w;
+      if (wave == 0) {
+        // lanes 0..3: slab k's and slab sb's L column k-1, tiles (k, k) and (sb, k) at version k-1
+        bool act = false;
+        const int* fp = flags;
+        int want = 0;
+        if (k > 0) {
+          const bool zero_rows = g.ident && sb == g.nbt + k;
+          if (lane == 0) { fp = pf_panel(flags, g, o, k - 1, 0); want = 1; act = true; }
+          if (lane == 1 && !zero_rows) { fp = pf_panel(flags, g, o, k - 1, sb - k); want = 1; act = true; }
+          if (lane == 2) { fp = pf_tver(flags, g, o, k, k); want = k - 1; act = true; }
+          if (lane == 3) { fp = pf_tver(flags, g, o, sb, k); want = max(k - 1 - p_s0(g, sb), 0); act = true; }
+        }
+        const bool ok = wave_wait(fp, want, act, abort_w);
+        if (lane == 0) red[15] = ok ? 1.0 : 0.0;
+        if (!ok && lane == 0) *habort = 1;                       // the host reruns the call
+      }
+      __syncthreads();
+      if (red[15] != 0.0) {
+        p_panel(A + (long long)o * g.ostride, g, o, k, w, part, status, Cs, colb, red);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // every storing wave drains
+        __syncthreads();
+        if (tid == 0) st_flag(pf_panel(flags, g, o, k, w), 1);
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- 4 tiles of step s = k - 1 (one per wave)
+    const int s = k - 1;
+    PTile tl;
+    bool have = false;
+    if (r < T1) {
+      const long long u = 4ll * r + wave;
+      if (u < (long long)g.n_obj * n1) {
+        have = true;
+        tl.o = (int)(u / n1);
+        const int i = (int)(u % n1);
+        tl.cb = k + 1;
+        tl.cpart = false;
+        tl.first = false;
+        if (!g.ident) tl.rb = k + 1 + i;
+        else tl.rb = i < g.nbt - k - 1 ? k + 1 + i : g.nbt + (i - (g.nbt - k - 1));
+      }
+    } else {
+      long long TL2, TC;
+      p_n2(g, k, TL2, TC);
+      const long long per = TL2 + TC;
+      const long long u = 4ll * (r - T1 - nP) + wave;
+      if (per > 0 && u < (long long)g.n_obj * per) {
+        have = true;
+        tl.o = (int)(u / per);
+        long long tt = u % per;
+        if (tt < TL2) {
+          const long long base = g.ident ? k + 1 : 2;
+          const double bb = 2.0 * (double)base - 1.0;
+          long long uu = (long long)((-bb + sqrt(bb * bb + 8.0 * (double)tt)) * 0.5);
+          if (uu < 0) uu = 0;
+          while (lpart_S(uu + 1, base) <= tt) ++uu;
+          while (lpart_S(uu, base) > tt) --uu;
+          const long long c = g.nbt - 1 - uu;
+          tl.cb = (int)c;
+          tl.rb = (int)(c + (tt - lpart_S(uu, base)));
+          tl.cpart = false;
+          tl.first = false;
+        } else {
+          tt -= TL2;
+          const int uu = tri_row(tt);
+          const int cp = k - 1 - uu;
+          const int b = cp + (int)(tt - (long long)uu * (uu + 1) / 2);
+          tl.rb = b;
+          tl.cb = cp;
+          tl.cpart = true;
+          tl.first = b == s;
+        }
+      }
+    }
+    // this wave's dependencies: L column s of both row blocks, the tile's previous version
+    bool ok = true;
+    if (have) {
+      const int* fp = flags;
+      int want = 0;
+      bool act = false;
+      const int sr = tl.cpart ? g.nbt + tl.rb : tl.rb, sc = tl.cpart ? g.nbt + tl.cb : tl.cb;
+      if (lane == 0) { fp = pf_panel(flags, g, tl.o, s, sr - s - 1); want = 1; act = true; }
+      if (lane == 1) { fp = pf_panel(flags, g, tl.o, s, sc - s - 1); want = 1; act = true; }
+      if (lane == 2 && !tl.first) {
+        fp = tl.cpart ? pf_tverc(flags, g, tl.o, tl.rb, tl.cb) : pf_tver(flags, g, tl.o, tl.rb, tl.cb);
+        want = tl.cpart ? s - tl.rb : s - p_s0(g, tl.rb);
+        act = true;
+      }
+      ok = wave_wait(fp, want, act, abort_w);
+      if (ok) p_tile_update(A, g, s, tl);
+    }
+    if (!ok && lane == 0) *habort = 1;                            // the host reruns the call
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // every storing wave drains
+    __syncthreads();
+    if (have && ok && lane == 0) {
+      // the tile's new version (steps applied), stored after the barrier that follows every
+      // wave's drain
+      int* vp = tl.cpart ? pf_tverc(flags, g, tl.o, tl.rb, tl.cb) : pf_tver(flags, g, tl.o, tl.rb, tl.cb);
+      st_flag(vp, tl.cpart ? s - tl.rb + 1 : s - p_s0(g, tl.rb) + 1);
+    }
+    __syncthreads();
+  }
+}
+
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 Geo make_geo(int n, int n_obj, bool ident) {
@@ -668,7 +1106,7 @@ int fit_factor(double* A, const Geo& g, const double* km, long long ld, const do
   const long long tiles = g.ident ? 2 * tri : tri + g.nbt;
   const long long blocks = g.n_obj * tiles + (g.ident ? 0 : g.n_obj);
   hipLaunchKernelGGL(fit_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s, A, g, (double*)km, ld,
-                     x, dim, y, ld_y, p, part, status, (int)tiles);
+                     x, dim, y, ld_y, p, part, status, (int)tiles, (int*)nullptr, 0ll);
   BO_CHECK_HIP(hipGetLastError());
   const int steps = g.ident ? g.nbt + 1 : g.nbt;
   for (int k = 0; k < steps; ++k) {
@@ -688,6 +1126,58 @@ int fit_factor(double* A, const Geo& g, const double* km, long long ld, const do
   }
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
 }
+
+// The persistent path: init launch (which also zeroes the flag words) + ONE fit_persist_kernel
+// launch.  BO_ERR_UNSUPPORTED when the task list exceeds PMAX_STEPS blocks (the caller uses
+// fit_factor).  *habort (host-visible) is set when a wait gave up: the caller reruns fit_factor.
+int fit_factor_persist(double* A, const Geo& g, const double* km, long long ld, const double* x, int dim,
+                       const double* y, long long ld_y, const FitParams& p, double* part, int* status,
+                       int* flags, int* habort, hipStream_t s) {
+  const int steps = g.ident ? g.nbt + 1 : g.nbt;
+  if (steps > PMAX_STEPS) return BO_ERR_UNSUPPORTED;
+  PPlan pl;
+  memset(&pl, 0, sizeof(pl));
+  pl.steps = steps;
+  long long tot = 0;
+  for (int k = 0; k < steps; ++k) {
+    pl.blk[k] = (int)tot;
+    const long long n1 = (k >= 1 && k + 1 < g.nbt) ? (g.ident ? g.nbt - 1 : g.nbt - k) : 0;
+    const long long np = k < g.nbt ? (g.ident ? g.nbt : g.nbt - k) : 0;
+    long long TL2 = 0, TC = 0;
+    if (k >= 1) {
+      const long long m2 = g.nbt - k - 2, base = g.ident ? k + 1 : 2;
+      TL2 = m2 > 0 ? m2 * base + m2 * (m2 - 1) / 2 : 0;
+      TC = g.ident ? (long long)k * (k + 1) / 2 : 0;
+    }
+    tot += (g.n_obj * n1 + 3) / 4 + g.n_obj * np + (g.n_obj * (TL2 + TC) + 3) / 4;
+  }
+  if (tot >= (1ll << 30)) return BO_ERR_UNSUPPORTED;
+  pl.blk[steps] = (int)tot;
+  pl.total = (int)tot;
+  const long long tri = (long long)g.nbt * (g.nbt + 1) / 2;
+  const long long tiles = g.ident ? 2 * tri : tri + g.nbt;
+  const long long work = g.n_obj * tiles + (g.ident ? 0 : g.n_obj);
+  const long long nf = p_flag_words(g);
+  const long long zb = (nf + 4095) / 4096;
+  hipLaunchKernelGGL(fit_init_kernel, dim3((unsigned)(work + zb)), dim3(256), 0, s, A, g, (double*)km, ld, x, dim,
+                     y, ld_y, p, part, status, (int)tiles, flags, nf);
+  BO_CHECK_HIP(hipGetLastError());
+  const unsigned grid = (unsigned)(tot < 256 ? tot : 256);
+  hipLaunchKernelGGL(fit_persist_kernel, dim3(grid), dim3(256), 0, s, A, g, pl, flags, part, status, habort);
+  return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
+}
+
+size_t flag_bytes(const Geo& g) { return a256((size_t)p_flag_words(g) * sizeof(int)); }
+
+// BO_FIT_PATH=launches forces the launch-per-step path (A/B measurements); read once
+bool persist_enabled() {
+  static const int on = [] {
+    const char* e = getenv("BO_FIT_PATH");
+    return (e && strcmp(e, "launches") == 0) ? 0 : 1;
+  }();
+  return on != 0;
+}
+long long g_fit_paths[3];     // persistent, launch-per-step, persistent aborted -> rerun
 
 // how often each inverse path ran (per objective; bo_invert_k_path_counts)
 long long g_inv_paths[3];     // Cholesky, blocked LU, Gauss-Jordan
@@ -715,11 +1205,16 @@ size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n) {
   const Geo g = make_geo((int)n, n_obj, true);
   // Gauss-Jordan scratch only above the blocked LU's capacity (the LU reuses the augmented region)
   const size_t lu = n > bo_lu_max_n() ? 2 * a256((size_t)n * n * sizeof(double)) : 0;
-  return geo_bytes(g) + lu + 2 * a256((size_t)n * sizeof(int)) + 512;
+  return geo_bytes(g) + lu + 2 * a256((size_t)n * sizeof(int)) + 512 + flag_bytes(g);
 }
 
 int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_t n, void* ws,
                 size_t ws_bytes, void* stream) {
+  return bo_invert_k_jitter(out, km, ld, n_obj, n, BO_KERNEL_JITTER, ws, ws_bytes, stream);   // numba_kernels.py:397-398
+}
+
+int bo_invert_k_jitter(double* out, const double* km, int64_t ld, int32_t n_obj, int64_t n, double jitter,
+                       void* ws, size_t ws_bytes, void* stream) {
   if (!out || !km || n_obj < 1 || n_obj > BO_MAX_OBJ || n < 1 || ld < n) return BO_ERR_ARG;
   if (n > (1 << 15)) return BO_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < bo_invert_k_workspace_size(n_obj, n)) return BO_ERR_WORKSPACE;
@@ -734,19 +1229,40 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
   int* piv = (int*)(lu + 2 * gj);
   int* perm = piv + a256((size_t)n * sizeof(int)) / sizeof(int);
   int* status = (int*)(lu + 2 * gj + 2 * a256((size_t)n * sizeof(int)));
-  BO_CHECK_HIP(hipMemsetAsync(status, 0, 256, s));
+  int* flags = (int*)(lu + 2 * gj + 2 * a256((size_t)n * sizeof(int)) + 512);
+  int* dabort = status + BO_MAX_OBJ + 2;          // set by the persistent kernel when a wait gave up
   FitParams p;
   memset(&p, 0, sizeof(p));
-  p.jitter = BO_KERNEL_JITTER;                 // numba_kernels.py:397-398
-  int st = fit_factor(A, g, km, ld, nullptr, 0, nullptr, 0, p, nullptr, status, s);
-  if (st != BO_OK) return st;
-  const unsigned nt = (unsigned)g.nbt;
-  hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, n_obj), dim3(256), 0, s, out, A, g, status);
-  BO_CHECK_HIP(hipGetLastError());
-  int* hstat = (int*)pinned(sizeof(int) * BO_MAX_OBJ);
+  p.jitter = jitter;
+  int* hstat = (int*)pinned(sizeof(int) * (BO_MAX_OBJ + 4));
   if (!hstat) return BO_ERR_HIP;
-  BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * n_obj, hipMemcpyDeviceToHost, s));
-  BO_CHECK_HIP(hipStreamSynchronize(s));
+  bool done = false;
+  if (persist_enabled()) {
+    BO_CHECK_HIP(hipMemsetAsync(status, 0, 256, s));
+    const int st = fit_factor_persist(A, g, km, ld, nullptr, 0, nullptr, 0, p, nullptr, status, flags, dabort, s);
+    if (st == BO_OK) {
+      const unsigned nt = (unsigned)g.nbt;
+      hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, n_obj), dim3(256), 0, s, out, A, g, status);
+      BO_CHECK_HIP(hipGetLastError());
+      BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * (BO_MAX_OBJ + 4), hipMemcpyDeviceToHost, s));
+      BO_CHECK_HIP(hipStreamSynchronize(s));
+      done = hstat[BO_MAX_OBJ + 2] == 0;
+      __atomic_fetch_add(&g_fit_paths[done ? 0 : 2], 1, __ATOMIC_RELAXED);
+    } else if (st != BO_ERR_UNSUPPORTED) {
+      return st;
+    }
+  }
+  if (!done) {
+    __atomic_fetch_add(&g_fit_paths[1], 1, __ATOMIC_RELAXED);
+    BO_CHECK_HIP(hipMemsetAsync(status, 0, 256, s));
+    int st = fit_factor(A, g, km, ld, nullptr, 0, nullptr, 0, p, nullptr, status, s);
+    if (st != BO_OK) return st;
+    const unsigned nt = (unsigned)g.nbt;
+    hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, n_obj), dim3(256), 0, s, out, A, g, status);
+    BO_CHECK_HIP(hipGetLastError());
+    BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * n_obj, hipMemcpyDeviceToHost, s));
+    BO_CHECK_HIP(hipStreamSynchronize(s));
+  }
   int fail[BO_MAX_OBJ];
   for (int o = 0; o < n_obj; ++o) {
     fail[o] = hstat[o];
@@ -759,7 +1275,7 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
     if (!fail[o]) continue;
     if (n <= bo_lu_max_n() && geo_bytes(g) >= bo_lu_workspace_size(n)) {
       const double* ko = km + (long long)o * ld * ld;
-      const int st2 = bo_lu_inverse(out + (long long)o * n * n, ko, ld, n, A, geo_bytes(g), s);
+      const int st2 = bo_lu_inverse(out + (long long)o * n * n, ko, ld, n, jitter, A, geo_bytes(g), s);
       __atomic_fetch_add(&g_inv_paths[1], 1, __ATOMIC_RELAXED);
       if (st2 != BO_OK) return st2;
       continue;
@@ -769,7 +1285,7 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
     BO_CHECK_HIP(hipMemsetAsync(gstat, 0, sizeof(int), s));
     const long long total = (long long)n * n;
     hipLaunchKernelGGL(jitter_copy_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       bufA, km, (long long)ld, (int)n, o, BO_KERNEL_JITTER);
+                       bufA, km, (long long)ld, (int)n, o, jitter);
     BO_CHECK_HIP(hipGetLastError());
     const int tiles = (int)((n + GJ_TILE - 1) / GJ_TILE);
     const size_t col_lds = (size_t)n * sizeof(double);
@@ -812,15 +1328,30 @@ int bo_invert_k_path_counts(int64_t* counts) {
   return BO_OK;
 }
 
+int bo_fit_path_counts(int64_t* counts) {
+  if (!counts) return BO_ERR_ARG;
+  for (int i = 0; i < 3; ++i) counts[i] = __atomic_load_n(&g_fit_paths[i], __ATOMIC_RELAXED);
+  return BO_OK;
+}
+
 size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n) {
   if (n_obj < 1 || n < 1) return 0;
   const Geo g = make_geo((int)n, n_obj, false);
-  return geo_bytes(g) + a256((size_t)n_obj * part_len(g) * sizeof(double) + BO_MAX_OBJ * sizeof(int)) + 512;
+  return geo_bytes(g) + a256((size_t)n_obj * part_len(g) * sizeof(double) + BO_MAX_OBJ * sizeof(int)) + 512 +
+         flag_bytes(g);
 }
 
 int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const double* y, int64_t ld_y,
                         double* km, int64_t ld, int32_t n_obj, const double* pm, const double* pv,
                         const double* ls, int64_t n, void* ws, size_t ws_bytes, void* stream) {
+  return bo_compute_mll_each_jitter(mll_obj, x, dim, y, ld_y, km, ld, n_obj, pm, pv, ls, n, BO_CHOLESKY_JITTER,
+                                    ws, ws_bytes, stream);   // numba_kernels.py:211-214
+}
+
+int bo_compute_mll_each_jitter(double* mll_obj, const double* x, int32_t dim, const double* y, int64_t ld_y,
+                               double* km, int64_t ld, int32_t n_obj, const double* pm, const double* pv,
+                               const double* ls, int64_t n, double jitter, void* ws, size_t ws_bytes,
+                               void* stream) {
   if (!mll_obj || !x || !y || !km || !pm || !pv || !ls || n_obj < 1 || n_obj > BO_MAX_OBJ ||
       n < 1 || ld < n || ld_y < n_obj || dim < 1)
     return BO_ERR_ARG;
@@ -832,12 +1363,14 @@ int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const dou
   // the per-step partials and the status flags go straight to pinned host memory (plain device
   // stores; visible after the stream synchronisation): no status memset and no read-back copy
   // per call -- two launches and their boundaries less per Powell evaluation
-  const size_t bytes = (size_t)n_obj * part_len(g) * sizeof(double) + sizeof(int) * n_obj;
+  const size_t bytes = (size_t)n_obj * part_len(g) * sizeof(double) + sizeof(int) * (n_obj + 1);
   double* h = (double*)pinned(bytes);
   if (!h) return BO_ERR_HIP;
   double* part = h;
   int* status = (int*)(part + (size_t)n_obj * part_len(g));
-  for (int o = 0; o < n_obj; ++o) status[o] = 0;
+  int* habort = status + n_obj;
+  int* flags = (int*)((char*)ws + geo_bytes(g) +
+                      a256((size_t)n_obj * part_len(g) * sizeof(double) + BO_MAX_OBJ * sizeof(int)) + 512);
   FitParams p;
   memset(&p, 0, sizeof(p));
   for (int o = 0; o < n_obj; ++o) {
@@ -845,10 +1378,26 @@ int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const dou
     p.pm[o] = pm[o];
     p.ls2[o] = ls[o] * ls[o];
   }
-  p.jitter = BO_CHOLESKY_JITTER;               // numba_kernels.py:211-214
-  int st = fit_factor(A, g, km, ld, x, dim, y, ld_y, p, part, status, s);
-  if (st != BO_OK) return st;
-  BO_CHECK_HIP(hipStreamSynchronize(s));
+  p.jitter = jitter;
+  bool done = false;
+  if (persist_enabled()) {
+    for (int o = 0; o <= n_obj; ++o) status[o] = 0;
+    const int st = fit_factor_persist(A, g, km, ld, x, dim, y, ld_y, p, part, status, flags, habort, s);
+    if (st == BO_OK) {
+      BO_CHECK_HIP(hipStreamSynchronize(s));
+      done = __atomic_load_n(habort, __ATOMIC_RELAXED) == 0;
+      __atomic_fetch_add(&g_fit_paths[done ? 0 : 2], 1, __ATOMIC_RELAXED);
+    } else if (st != BO_ERR_UNSUPPORTED) {
+      return st;
+    }
+  }
+  if (!done) {
+    __atomic_fetch_add(&g_fit_paths[1], 1, __ATOMIC_RELAXED);
+    for (int o = 0; o < n_obj; ++o) status[o] = 0;
+    const int st = fit_factor(A, g, km, ld, x, dim, y, ld_y, p, part, status, s);
+    if (st != BO_OK) return st;
+    BO_CHECK_HIP(hipStreamSynchronize(s));
+  }
   const int* hstat = (const int*)(h + (size_t)n_obj * part_len(g));
   for (int o = 0; o < n_obj; ++o)
     if (hstat[o]) return BO_ERR_NOT_PD;

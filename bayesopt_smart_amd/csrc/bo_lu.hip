@@ -393,8 +393,8 @@ size_t bo_lu_workspace_size(int64_t n) {
 
 int bo_lu_max_n() { return LT * LR; }
 
-int bo_lu_inverse(double* out, const double* km, int64_t ld, int64_t n, void* ws, size_t ws_bytes,
-                  hipStream_t s) {
+int bo_lu_inverse(double* out, const double* km, int64_t ld, int64_t n, double jitter, void* ws,
+                  size_t ws_bytes, hipStream_t s) {
   if (n < 1 || n > LT * LR) return BO_ERR_UNSUPPORTED;
   if (ws_bytes < bo_lu_workspace_size(n)) return BO_ERR_WORKSPACE;
   const LuGeo g = make_lu_geo((int)n);
@@ -404,7 +404,7 @@ int bo_lu_inverse(double* out, const double* km, int64_t ld, int64_t n, void* ws
   BO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
   const unsigned tiles = (unsigned)((g.n_p + 31) / 32);
   hipLaunchKernelGGL(lu_init_kernel, dim3(tiles, tiles), dim3(256), 0, s, A, g, km, (long long)ld,
-                     BO_KERNEL_JITTER);
+                     jitter);
   for (int k = 0; k < g.nbs; ++k) {
     const int blocks = k > 0 ? g.nbs - k : 1;      // the panel + the strips right of it
     hipLaunchKernelGGL(lu_step_kernel, dim3(blocks), dim3(LT), 0, s, A, g, k, ipiv, status);

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256, 1) void kmem_predict_kernel(const FusedArgs a)
       if (valid && g == 0) {
         const long long off = (long long)o * a.ld_out + j;
         if (a.mu) a.mu[off] = a.pm[o] + mpart;                      // :486-488
-        if (a.var) a.var[off] = fmax(pv - qpart, BO_MIN_VARIANCE);  // :532-535
+        if (a.var) a.var[off] = fmax(pv - qpart, a.min_var);  // :532-535
       }
     }
   }
@@ -476,7 +476,7 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
     return BO_ERR_ARG;
   if (d->n_train < 1 || d->n_cand < 0 || d->topq < 0 || d->topq > BO_MAX_TOPQ) return BO_ERR_ARG;
   if (d->cand_kind < 0 || d->cand_kind > BO_CAND_SOBOL) return BO_ERR_ARG;
-  if (d->mode & ~(BO_PREDICT_DENSE | BO_PREDICT_NO_SEPARABLE | BO_PREDICT_FP32)) return BO_ERR_ARG;
+  if (d->mode & ~(BO_PREDICT_DENSE | BO_PREDICT_NO_SEPARABLE | BO_PREDICT_FP32 | BO_PREDICT_F32_FLOOR)) return BO_ERR_ARG;
   if (d->excl_points && d->n_excl < 0) return BO_ERR_ARG;
   const long long n = d->n_train;
   if (n > (1 << 14)) return BO_ERR_UNSUPPORTED;
@@ -703,6 +703,7 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     fa.inv_rsq_pv[o] = 1.0 / sqrt(d->prior_var[o]);
     fa.inv_pv[o] = 1.0 / d->prior_var[o];
   }
+  fa.min_var = (d->mode & BO_PREDICT_F32_FLOOR) ? BO_MIN_VARIANCE_F32 : BO_MIN_VARIANCE;
   fa.mu = d->mu;
   fa.var = d->var;
   fa.std_mu = d->std_mu;

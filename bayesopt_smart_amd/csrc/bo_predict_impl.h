@@ -45,6 +45,7 @@ struct FusedArgs {
   const double* alpha;                   // [n_obj][n_pad] = K^-1 (y - pm) (global)
   double pm[BO_MAX_OBJ], pv[BO_MAX_OBJ], nhl[BO_MAX_OBJ], beta[BO_MAX_OBJ];
   double inv_rsq_pv[BO_MAX_OBJ], inv_pv[BO_MAX_OBJ];   // 1 / sqrt(pv), 1 / pv (epilogue multiplies)
+  double min_var;                        // MIN_VARIANCE (config.py:57-66): 1e-10, or 1e-6 (F32_FLOOR)
   int idx32;                             // grid: every linear index and extent below 2^31
   double *mu, *var, *std_mu, *std_var, *ucb, *acq;
   TopEntry* partial;                     // [gridDim.x * kWaves][topq]
@@ -657,7 +658,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       mpart += __shfl_xor(mpart, 32, 64);
       const double pv = a.pv[o], pm = a.pm[o];
       const double mu = pm + mpart;                                   // :486-488
-      const double var = fmax(pv - qpart, BO_MIN_VARIANCE);           // :532-535
+      const double var = fmax(pv - qpart, a.min_var);                 // :532-535
 #ifdef BO_ABL_NOEPI
       const double smu = mu - pm, svar = var, u = smu + a.beta[o] * svar;
 #else
@@ -967,7 +968,7 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
       mpart += __shfl_xor(mpart, 32, 64);
       const double pv = a.pv[o], pm = a.pm[o];
       const double mu = pm + (double)mpart;                               // :486-488
-      const double var = fmax(pv - 2.0 * (double)qpart, BO_MIN_VARIANCE);  // :532-535
+      const double var = fmax(pv - 2.0 * (double)qpart, a.min_var);  // :532-535
       const double smu = (mu - pm) * a.inv_rsq_pv[o];                     // :563-565 (x 1/sqrt(pv))
       const double svar = var * a.inv_pv[o];                              // :568-570 (x 1/pv)
       const double u = smu + a.beta[o] * sqrt(fabs(svar));                // acquisition.py:52

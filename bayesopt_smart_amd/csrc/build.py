@@ -20,7 +20,8 @@ LIB = os.path.join(PKG, f"libbo_amd{('_' + VARIANT.lower().replace(',', '_')) if
 BUILD = os.path.join(HERE, "build" + (("_" + VARIANT.lower()) if VARIANT else ""))
 SOURCES = ["bo_predict_d2.hip", "bo_predict_d4.hip", "bo_predict_d6.hip", "bo_predict_d8.hip",
            "bo_predict_s2.hip", "bo_predict_s4.hip", "bo_predict_s6.hip", "bo_predict_s8.hip",
-           "bo_predict.hip", "bo_fit.hip", "bo_lu.hip", "bo_select.hip", "bo_misc.hip", "bo_hvi.hip"]
+           "bo_predict.hip", "bo_fit.hip", "bo_lu.hip", "bo_select.hip", "bo_misc.hip", "bo_hvi.hip",
+           "bo_powell.hip"]
 HEADERS = ["bo_common.h", "bo_predict_impl.h", os.path.join("..", "..", "include", "bo_amd.h")]
 ARCH = os.environ.get("BO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",

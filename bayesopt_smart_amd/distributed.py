@@ -33,6 +33,9 @@ def exchange_topq_rec(rec, q, group=None, out=None):
     identical on every rank: NaN first, then descending value, ties by ascending index.
     """
     world = dist.get_world_size(group)
+    if dist.get_backend(group) != "nccl" and rec.device.type != "cpu":
+        rec = rec.cpu()                         # gloo ranks (CPU collectives) on one device
+        out = None
     g = out if out is not None else torch.empty(world * 2 * q, dtype=rec.dtype, device=rec.device)
     dist.all_gather_into_tensor(g, rec.contiguous(), group=group)
     g = g.view(world, 2 * q)
@@ -84,6 +87,8 @@ def front_hypervolume(front, reference_point, group=None, device=None, partial=N
         _lib.check(_lib.load().bo_box_volume_sum(bd.data_ptr() if bd.numel() else None, mine.shape[0], r.size,
                                                  ub, val.data_ptr(), stream_handle(dev)), "bo_box_volume_sum")
     if world > 1:
+        if dist.get_backend(group) != "nccl":
+            val = val.cpu()
         dist.all_reduce(val, op=dist.ReduceOp.SUM, group=group)
     return float(np.prod(upper - r) - val.item())
 
@@ -107,7 +112,7 @@ def gather_shards(t, n, group=None):
 
 def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
                             betas, q, outputs=("acq",), group=None, device=None, scorer=None, out=None,
-                            mode="auto"):
+                            mode="auto", float_type=None):
     """Score this rank's shard of `cands` and return (local results, global top-q).
 
     Rank r scores candidates shard_range(M, r, P) (its outputs, [n_obj, count] / [count], go to
@@ -132,6 +137,7 @@ def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_var
         kw["out"] = out
     if scorer is None:
         kw["mode"] = mode
+        kw["float_type"] = float_type
     r = score(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales, betas,
               outputs=outputs, topq=q, offset=off, count=cnt, **kw)
     if world == 1:

@@ -3,8 +3,13 @@
 Same names, argument meaning, in-place conventions and error behaviour as the reference
 functions; the arithmetic runs in libbo_amd.so kernels.  Arrays may be numpy arrays (as the
 reference passes them: results are copied back in place) or HIP device tensors (no host
-round trip).  Only the hyper-parameter optimiser driver (scipy Powell, a sequential host
-algorithm) and the initial LHS design stay on the host, as SURVEY.md §2 scopes them.
+round trip).  The hyper-parameter optimiser driver (Powell, a sequential host algorithm) runs
+natively in the library around the device MLL (bo_optimize_hyperparams_mll, a restatement of
+scipy's Powell); the initial LHS design stays on the host, as SURVEY.md §2 scopes it.
+
+``float_type`` (keyword; default config.NUMBA_FLOAT_TYPE at call time): np.float32 selects the
+reference's float32 branch (config.py:57-66 jitters, COBYLA for the fit, numba_kernels.py:290-302);
+the device arithmetic stays binary64.
 """
 
 from __future__ import annotations
@@ -16,8 +21,11 @@ import torch
 from scipy.optimize import minimize
 
 from . import _lib
+from scipy.optimize import OptimizeResult
+
 from .config import (HYPERPARAM_FTOL, HYPERPARAM_MAXITER, HYPERPARAM_METHOD,
-                     HYPERPARAM_MIN_BOUND, HYPERPARAM_XTOL, NUMBA_FLOAT_TYPE)
+                     HYPERPARAM_MIN_BOUND, HYPERPARAM_XTOL, NUMBA_FLOAT_TYPE, precision_constants,
+                     resolve_float_type)
 from .device import F64, Workspace, require_device, stream_handle
 
 
@@ -113,8 +121,9 @@ def update_k(kernel_matrix, x_vector, last_eval, current_eval, prior_variance, l
     km.finish()
 
 
-def invert_k(current_eval, kernel_matrix):
-    """numba_kernels.py:370-403 — inv(K[:N,:N] + 1e-6 I) per objective (LU-class pivoting).
+def invert_k(current_eval, kernel_matrix, *, float_type=None):
+    """numba_kernels.py:370-403 — inv(K[:N,:N] + KERNEL_JITTER I) per objective (1e-6; 1e-3 in the
+    float32 branch): Cholesky, or the blocked LU with partial pivoting when it fails.
 
     Returns a new array of the caller's kind (numpy in, numpy out; tensor in, tensor out).
     Raises numpy.linalg.LinAlgError on an exactly singular pivot.
@@ -126,16 +135,17 @@ def invert_k(current_eval, kernel_matrix):
     out = torch.empty((n_obj, n, n), dtype=F64, device=dev)
     lib = _lib.load()
     ws = Workspace.get(lib.bo_invert_k_workspace_size(n_obj, n), dev)
-    _lib.check(lib.bo_invert_k(out.data_ptr(), km.ptr, ld, n_obj, n, ws.data_ptr(), ws.numel(),
-                               stream_handle(dev)), "bo_invert_k")
+    jitter = precision_constants(float_type)[0]
+    _lib.check(lib.bo_invert_k_jitter(out.data_ptr(), km.ptr, ld, n_obj, n, jitter, ws.data_ptr(), ws.numel(),
+                                      stream_handle(dev)), "bo_invert_k")
     return out if isinstance(kernel_matrix, torch.Tensor) else out.cpu().numpy()
 
 
 def compute_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance, length_scales,
-                current_eval):
+                current_eval, *, float_type=None):
     """numba_kernels.py:152-235 — summed marginal log likelihood (Gram rebuilt in place).
 
-    Raises numpy.linalg.LinAlgError when K/pv + 1e-8 I is not positive definite (:214).
+    Raises numpy.linalg.LinAlgError when K/pv + CHOLESKY_JITTER I is not positive definite (:214).
     """
     dev = _dev_of(kernel_matrix, x_vector, y_vector)
     km = _Arg(kernel_matrix, dev, write=True)
@@ -145,17 +155,20 @@ def compute_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance, l
     n = int(current_eval)
     lib = _lib.load()
     ws = Workspace.get(lib.bo_compute_mll_workspace_size(n_obj, n), dev)
-    out = C.c_double()
-    st = lib.bo_compute_mll(C.byref(out), x.ptr, x.t.shape[1], y.ptr, y.t.stride(0), km.ptr, ld, n_obj,
-                            _host_vec(prior_mean, n_obj), _host_vec(prior_variance, n_obj),
-                            _host_vec(length_scales, n_obj), n, ws.data_ptr(), ws.numel(),
-                            stream_handle(dev))
+    out = (C.c_double * n_obj)()
+    st = lib.bo_compute_mll_each_jitter(out, x.ptr, x.t.shape[1], y.ptr, y.t.stride(0), km.ptr, ld, n_obj,
+                                        _host_vec(prior_mean, n_obj), _host_vec(prior_variance, n_obj),
+                                        _host_vec(length_scales, n_obj), n, precision_constants(float_type)[1],
+                                        ws.data_ptr(), ws.numel(), stream_handle(dev))
     km.finish()
     _lib.check(st, "bo_compute_mll")
-    return out.value
+    tot = 0.0
+    for o in range(n_obj):                      # np.sum over the objectives (:235): sequential, < 8 terms
+        tot += out[o]
+    return tot
 
 
-def _mll_terms(xd, yd, km, prior_mean, prior_variance, length_scales, n, objs):
+def _mll_terms(xd, yd, km, prior_mean, prior_variance, length_scales, n, objs, jitter=1e-8):
     """Per-objective MLL terms (bo_compute_mll_each) of the objectives `objs` (device arrays;
     one call over all objectives, or one single-objective call for one of them)."""
     lib = _lib.load()
@@ -169,19 +182,69 @@ def _mll_terms(xd, yd, km, prior_mean, prior_variance, length_scales, n, objs):
     out = (C.c_double * cnt)()
     ws = Workspace.get(lib.bo_compute_mll_workspace_size(cnt, n), dev)
     sel = lambda v: _host_vec(np.asarray(v, dtype=np.float64)[o0:o0 + cnt], cnt)  # noqa: E731
-    st = lib.bo_compute_mll_each(out, xd.data_ptr(), xd.shape[1], yd.data_ptr() + 8 * o0, yd.stride(0),
-                                 km.data_ptr() + 8 * o0 * ld * ld, ld, cnt, sel(prior_mean),
-                                 sel(prior_variance), sel(length_scales), n, ws.data_ptr(), ws.numel(),
-                                 stream_handle(dev))
+    st = lib.bo_compute_mll_each_jitter(out, xd.data_ptr(), xd.shape[1], yd.data_ptr() + 8 * o0, yd.stride(0),
+                                        km.data_ptr() + 8 * o0 * ld * ld, ld, cnt, sel(prior_mean),
+                                        sel(prior_variance), sel(length_scales), n, jitter, ws.data_ptr(),
+                                        ws.numel(), stream_handle(dev))
     _lib.check(st, "bo_compute_mll_each")
     return {o0 + i: out[i] for i in range(cnt)}
 
 
+_POWELL_MESSAGES = {0: "Optimization terminated successfully.",
+                    1: "Maximum number of function evaluations has been exceeded.",
+                    2: "Maximum number of iterations has been exceeded.",
+                    3: "NaN result encountered.",
+                    4: "The result is outside of the provided bounds."}
+
+
+def _powell_result(x, r, direc):
+    return OptimizeResult(fun=float(r.fun), direc=direc, nit=int(r.nit), nfev=int(r.nfev),
+                          status=int(r.warnflag), success=r.warnflag == 0,
+                          message=_POWELL_MESSAGES.get(int(r.warnflag), ""), x=x)
+
+
+def powell_minimize(fun, x0, bounds, xtol=1e-4, ftol=1e-4, maxiter=None, maxfev=None):
+    """``scipy.optimize.minimize(fun, x0, method="Powell", bounds=bounds, options=...)`` on the
+    library's native driver (bo_powell_minimize: scipy 1.15's algorithm restated in C++; tan/atan
+    from the C library).  `bounds`: sequence of (lo, hi) pairs, None = unbounded.  Returns an
+    OptimizeResult like scipy's; an exception raised by `fun` propagates."""
+    x = np.array(x0, dtype=np.float64).ravel()
+    n = x.size
+    lb = np.array([-np.inf if b[0] is None else b[0] for b in bounds], dtype=np.float64)
+    ub = np.array([np.inf if b[1] is None else b[1] for b in bounds], dtype=np.float64)
+    err = []
+
+    def cb(xp, nn, fp, _user):
+        try:
+            fp[0] = float(fun(np.ctypeslib.as_array(xp, shape=(nn,)).copy()))
+            return 0
+        except BaseException as exc:   # re-raised below; the driver stops at the non-zero status
+            err.append(exc)
+            return 100
+    cfun = _lib.OBJECTIVE_FN(cb)
+    res = _lib.PowellResult()
+    direc = np.zeros((n, n))
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    st = _lib.load().bo_powell_minimize(cfun, None, dp(x), n, dp(lb), dp(ub), float(xtol), float(ftol),
+                                        -1 if maxiter is None else int(maxiter),
+                                        -1 if maxfev is None else int(maxfev), dp(direc), C.byref(res))
+    if err:
+        raise err[0]
+    _lib.check(st, "bo_powell_minimize")
+    return _powell_result(x, res, direc)
+
+
 def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance,
-                             length_scales, current_eval, memo=True):
-    """numba_kernels.py:238-321 — Powell over [ls..., var...] (bounds >= 1e-5) maximising the
-    device MLL; updates length_scales and prior_variance in place, returns the OptimizeResult.
-    The training arrays are staged on the device once for all ~100-200 MLL evaluations.
+                             length_scales, current_eval, memo=True, *, float_type=None, driver="native"):
+    """numba_kernels.py:238-321 — maximise the device MLL over [ls..., var...] (bounds >= 1e-5);
+    updates length_scales and prior_variance in place, returns the OptimizeResult.  The training
+    arrays are staged on the device once for all ~100-300 MLL evaluations.
+
+    float64 (the reference's default branch): Powell (:305-315).  driver "native" (default) runs
+    the whole fit as ONE library call, bo_optimize_hyperparams_mll: the Powell driver in C++ around
+    the device MLL, no Python per evaluation; driver "scipy" runs scipy's Powell over the same
+    device terms (the pre-round-4 path, kept for comparison).  float32 (:290-302): scipy's COBYLA
+    with rhobeg 1.0 and tol 10 ftol over the MLL with the float32 jitter.
 
     `memo`: the MLL is a sum of per-objective terms, each a function of (x, y, pm, ls_o) only --
     the correlation matrix K / pv does not depend on pv (:195-198; the device builds it pv-free) --
@@ -191,6 +254,8 @@ def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prio
     device arithmetic), so Powell's path is unchanged; evaluations that move only pv need no
     device call (about half of them).  kernel_matrix ends as the reference leaves it: the Gram of
     the last evaluated hyper-parameters."""
+    ft = resolve_float_type(float_type)
+    _, chol_jitter, _ = precision_constants(ft)
     dev = _dev_of(kernel_matrix, x_vector, y_vector)
     n_obj = np.asarray(length_scales).shape[0] if not isinstance(length_scales, torch.Tensor) \
         else length_scales.shape[0]
@@ -201,29 +266,60 @@ def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prio
     pv0 = prior_variance.cpu().numpy() if isinstance(prior_variance, torch.Tensor) else np.asarray(prior_variance)
     pm = np.asarray(prior_mean.cpu().numpy() if isinstance(prior_mean, torch.Tensor) else prior_mean,
                     dtype=np.float64)
-    initial_guess = np.concatenate([ls0, pv0])
+    n = int(current_eval)
+    lib = _lib.load()
+    if ft == np.float64 and driver == "native" and memo and HYPERPARAM_METHOD == "Powell":
+        ls_io = np.array(ls0, dtype=np.float64)
+        pv_io = np.array(pv0, dtype=np.float64)
+        pm_c = np.ascontiguousarray(pm[:n_obj])
+        ws = Workspace.get(lib.bo_compute_mll_workspace_size(n_obj, n), dev)
+        res = _lib.PowellResult()
+        direc = np.zeros((2 * n_obj, 2 * n_obj))
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        st = lib.bo_optimize_hyperparams_mll(
+            xd.data_ptr(), xd.shape[1], yd.data_ptr(), yd.stride(0), km.ptr, km.t.shape[-1], n_obj, dp(pm_c),
+            dp(pv_io), dp(ls_io), n, chol_jitter, HYPERPARAM_XTOL, HYPERPARAM_FTOL, HYPERPARAM_MAXITER,
+            HYPERPARAM_MIN_BOUND, ws.data_ptr(), ws.numel(), stream_handle(dev), C.byref(res), dp(direc))
+        if st != _lib.ERR_UNSUPPORTED:
+            km.finish()
+            _lib.check(st, "bo_optimize_hyperparams_mll")
+            out = _powell_result(np.concatenate([ls_io, pv_io]), res, direc)
+            out.device_calls = int(res.device_calls)
+            _assign(length_scales, ls_io)
+            _assign(prior_variance, pv_io)
+            return out
+        # a line search unbounded in both directions (not produced by these bounds): scipy's driver
+    initial_guess = np.concatenate([ls0, pv0]).astype(np.float64)
     bounds = [(HYPERPARAM_MIN_BOUND, None)] * (2 * n_obj)
     cache = [dict() for _ in range(n_obj)]
     last = [None]
+    calls = [0]
 
     def objective(params):
         ls, pv = params[:n_obj], params[n_obj:]
         last[0] = params.copy()
         if not memo:
-            return -compute_mll(xd, yd, km.t, pm, pv, ls, current_eval)
+            calls[0] += 1
+            return -compute_mll(xd, yd, km.t, pm, pv, ls, current_eval, float_type=ft)
         todo = [o for o in range(n_obj) if float(ls[o]) not in cache[o]]
         if todo:
             objs = todo if len(todo) == 1 else list(range(n_obj))
-            for o, v in _mll_terms(xd, yd, km.t, pm, pv, ls, current_eval, objs).items():
+            calls[0] += 1
+            for o, v in _mll_terms(xd, yd, km.t, pm, pv, ls, current_eval, objs, chol_jitter).items():
                 cache[o][float(ls[o])] = v
         tot = 0.0
         for o in range(n_obj):                  # np.sum over < 8 terms: sequential (:235)
             tot += cache[o][float(ls[o])]
         return -tot
 
-    res = minimize(objective, initial_guess, method=HYPERPARAM_METHOD, bounds=bounds,
-                   options={"xtol": HYPERPARAM_XTOL, "ftol": HYPERPARAM_FTOL,
-                            "maxiter": HYPERPARAM_MAXITER})
+    if ft == np.float32:                        # numba_kernels.py:290-302
+        res = minimize(objective, initial_guess, method="COBYLA", bounds=bounds,
+                       options={"maxiter": HYPERPARAM_MAXITER, "rhobeg": 1.0, "tol": HYPERPARAM_FTOL * 10})
+    else:
+        res = minimize(objective, initial_guess, method=HYPERPARAM_METHOD, bounds=bounds,
+                       options={"xtol": HYPERPARAM_XTOL, "ftol": HYPERPARAM_FTOL,
+                                "maxiter": HYPERPARAM_MAXITER})
+    res.device_calls = calls[0]
     if memo and last[0] is not None:            # the reference's compute_mll side effect
         update_k(km.t, xd, 0, current_eval, last[0][n_obj:], last[0][:n_obj])
     km.finish()

@@ -170,7 +170,7 @@ MODES = {"auto": 0, "dense": 1, "auto-exp": 2, "dense-exp": 3, "fp32": 4}
 def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, prior_variance,
                     length_scales, betas, *, outputs=("mu", "var", "acq"), topq=0,
                     excl_points=None, offset=0, count=None, out=None, device=None, mode="auto",
-                    top_rec=None, prepare=False):
+                    top_rec=None, prepare=False, float_type=None):
     """Score candidates [offset, offset+count) of `cands`.
 
     x_train [N, d], y_train [N or T, n_obj] (only the first N rows are read), kinv
@@ -193,6 +193,9 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
 
     ``prepare=True`` returns a PreparedPredict instead of launching: calling it launches this
     call again (same buffers), without re-validating.
+
+    ``float_type`` (default config.NUMBA_FLOAT_TYPE): np.float32 applies the reference's float32
+    branch's variance floor MIN_VARIANCE = 1e-6 (config.py:57-61; BO_PREDICT_F32_FLOOR).
     """
     dev = require_device(device)
     x_train = as_dev(x_train, dev)
@@ -212,7 +215,8 @@ def predict_acquire(x_train, y_train, kinv, cands: CandidateSet, prior_mean, pri
         raise ValueError(f"topq must be in [0, {_lib.MAX_TOPQ}]")
     desc = _fill_desc(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales,
                       betas, offset, count, excl_points, topq)
-    desc.mode = MODES[mode]
+    from .config import resolve_float_type
+    desc.mode = MODES[mode] | (_lib.MODE_F32_FLOOR if resolve_float_type(float_type) == np.float32 else 0)
     res = {} if out is None else dict(out)
     for name in outputs:
         if name not in OUTPUT_NAMES:

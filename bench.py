@@ -331,11 +331,20 @@ def run_fit(cfg, label, dev):
     ref_lu = np.linalg.inv(km_lu[0].cpu().numpy() + 1e-6 * np.eye(n))
     lu_err = float(np.abs(kinv_lu[0].cpu().numpy() - ref_lu).max() / np.abs(ref_lu).max())
     ls_fit, pv_fit = ls.copy(), pv.copy()
+    paths0 = bo._lib.fit_path_counts()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = bo.kernels.optimize_hyperparams_mll(xd, yd, km, pm, pv_fit, ls_fit, n)
     torch.cuda.synchronize()
     fit_ms = (time.perf_counter() - t0) * 1e3
+    paths1 = bo._lib.fit_path_counts()
+    # the same fit with scipy's Powell driver over the same device terms (the round-3 path)
+    ls_s, pv_s = ls.copy(), pv.copy()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res_s = bo.kernels.optimize_hyperparams_mll(xd, yd, km, pm, pv_s, ls_s, n, driver="scipy")
+    torch.cuda.synchronize()
+    fit_scipy_ms = (time.perf_counter() - t0) * 1e3
     return {
         "metric": f"GP fit on device (Gram + inverse, MLL evaluation, Powell fit), {label}",
         "value": fit_ms, "unit": "ms per Powell hyper-parameter fit", "higher_is_better": False,
@@ -349,6 +358,12 @@ def run_fit(cfg, label, dev):
         "compute_mll_ms": mll_ms, "mll": mll, "mll_lapack": mll_ref,
         "mll_rel_err": abs(mll - mll_ref) / max(1.0, abs(mll_ref)),
         "powell_nfev": int(res.nfev), "powell_ms_per_eval": fit_ms / max(int(res.nfev), 1),
+        "powell_device_calls": int(getattr(res, "device_calls", -1)),
+        "powell_driver": "native (bo_optimize_hyperparams_mll: one library call)",
+        "powell_scipy_driver_ms": fit_scipy_ms,
+        "powell_scipy_driver_same_result": bool(np.array_equal(res.x, res_s.x) and res.nfev == res_s.nfev),
+        "factorisation_schedule": os.environ.get("BO_FIT_PATH", "persistent"),
+        "fit_paths_during_powell": {k: paths1[k] - paths0[k] for k in paths1},
         "fitted_length_scales": ls_fit.tolist(),
     }
 

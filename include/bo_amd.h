@@ -13,7 +13,9 @@
  *     asynchronous on that stream unless stated otherwise;
  *   - the return value is a bo_status; no C++ exception crosses the ABI.
  *   - all floating point is IEEE binary64 (the reference's NUMBA_FLOAT_TYPE,
- *     bayesopt/config.py:54).
+ *     bayesopt/config.py:54); the reference's float32 branch (config.py:57-61: jitters 1e-3 /
+ *     1e-4, variance floor 1e-6) is reachable through the *_jitter entry points and
+ *     BO_PREDICT_F32_FLOOR.
  */
 #ifndef BO_AMD_H
 #define BO_AMD_H
@@ -25,7 +27,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 2
+#define BO_ABI_VERSION 3
 #define BO_MAX_OBJ 8      /* objectives per call                              */
 #define BO_MAX_DIM 8      /* input dimensions                                 */
 #define BO_MAX_TOPQ 48    /* batch size of the fused top-q selection          */
@@ -98,11 +100,14 @@ int bo_device_count(void);
  * check"): K* and the upper-form contraction in f32 on v_mfma_f32_16x16x4_f32, the mean and
  * quadratic form accumulated in f32, everything after them in f64; every candidate evaluates
  * exp (no grid table); DENSE / NO_SEPARABLE are ignored with it. */
+/* BO_PREDICT_F32_FLOOR: the posterior variance floor of the reference's float32 branch,
+ * MIN_VARIANCE = 1e-6 (config.py:57-61), instead of the fp64 branch's 1e-10 (:63-66). */
 typedef enum bo_predict_mode {
   BO_PREDICT_AUTO = 0,
   BO_PREDICT_DENSE = 1,
   BO_PREDICT_NO_SEPARABLE = 2,
-  BO_PREDICT_FP32 = 4
+  BO_PREDICT_FP32 = 4,
+  BO_PREDICT_F32_FLOOR = 8
 } bo_predict_mode;
 
 typedef struct bo_predict_desc {
@@ -265,7 +270,16 @@ int bo_invert_k(double* out, const double* kernel_matrix, int64_t ld, int32_t n_
  * N <= 2048), [2] Gauss-Jordan (the same above N = 2048).  Diagnostics for the fallback's
  * frequency. */
 int bo_invert_k_path_counts(int64_t* counts);
+/* bo_invert_k with the diagonal jitter given: KERNEL_JITTER of config.py:57-66 (1e-6 in the fp64
+ * branch, which bo_invert_k uses; 1e-3 in the float32 branch). */
+int bo_invert_k_jitter(double* out, const double* kernel_matrix, int64_t ld, int32_t n_obj, int64_t n,
+                       double jitter, void* workspace, size_t workspace_bytes, void* stream);
 size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n);
+/* Process-wide counts of the factorisation schedules bo_invert_k / bo_compute_mll* ran:
+ * counts[0] the persistent launch (one task-queue kernel: panels and trailing-update tiles hand
+ * off through flags), [1] one launch per 32-column step (N > 4064, or BO_FIT_PATH=launches),
+ * [2] persistent launches that gave up a wait (bounded spin) and were rerun step by step. */
+int bo_fit_path_counts(int64_t* counts);
 
 /* compute_mll  bayesopt/numba_kernels.py:152-235 (Gram rebuilt into kernel_matrix first, as
  * the reference does).  Writes the summed MLL to *mll_out (host).  Returns BO_ERR_NOT_PD when
@@ -282,7 +296,48 @@ int bo_compute_mll_each(double* mll_obj, const double* x, int32_t dim, const dou
                         double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
                         const double* prior_var, const double* length_scale, int64_t n,
                         void* workspace, size_t workspace_bytes, void* stream);
+/* bo_compute_mll_each with the correlation matrix's jitter given: CHOLESKY_JITTER of
+ * config.py:57-66 (1e-8 in the fp64 branch, which bo_compute_mll_each uses; 1e-4 in float32). */
+int bo_compute_mll_each_jitter(double* mll_obj, const double* x, int32_t dim, const double* y, int64_t ld_y,
+                               double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
+                               const double* prior_var, const double* length_scale, int64_t n, double jitter,
+                               void* workspace, size_t workspace_bytes, void* stream);
 size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n);
+
+/* ------------------------------------------------------------------------------------
+ * The fit's driver, native (HOST code calling the device MLL): scipy.optimize.minimize(
+ * method="Powell", bounds=...) as optimize_hyperparams_mll calls it (numba_kernels.py:238-321,
+ * :305-315), restated from scipy 1.15's _minimize_powell / _linesearch_powell / _line_for_search /
+ * _minimize_scalar_bounded operation for operation (tan/atan from the C library).
+ * ---------------------------------------------------------------------------------- */
+/* objective: *f = f(x[0..n)); a non-zero return aborts the minimisation with that status */
+typedef int (*bo_objective_fn)(const double* x, int32_t n, double* f, void* user);
+typedef struct bo_powell_result {
+  double fun;             /* final objective value                                          */
+  int64_t nfev;           /* objective evaluations                                          */
+  int64_t nit;            /* Powell iterations                                              */
+  int64_t device_calls;   /* bo_optimize_hyperparams_mll: device MLL calls (memo misses)     */
+  int32_t warnflag;       /* scipy's status: 0 success, 1 maxfev, 2 maxiter, 3 nan, 4 bounds  */
+  int32_t reserved;
+} bo_powell_result;
+/* Minimise fn from x (in: x0, out: the result) within lb <= x <= ub (host [n]; +-inf allowed);
+ * maxiter / maxfev < 0 = None (scipy's defaults).  direc (optional, host [n][n]) receives the
+ * final direction set.  BO_ERR_UNSUPPORTED when a line search is unbounded in both directions
+ * (scipy's bracketing Brent; the fit's bounds never need it). */
+int bo_powell_minimize(bo_objective_fn fn, void* user, double* x, int32_t n, const double* lb,
+                       const double* ub, double xtol, double ftol, int64_t maxiter, int64_t maxfev,
+                       double* direc, bo_powell_result* res);
+/* optimize_hyperparams_mll (numba_kernels.py:238-321) as ONE call: Powell over [ls..., pv...] from
+ * the given values (host, updated in place on success), bounds [min_bound, inf), maximising the
+ * device MLL (bo_compute_mll_each_jitter; each per-objective term memoised per distinct ls_o, a
+ * device call only for the objectives whose ls changed).  kernel_matrix ends as the Gram of the
+ * last evaluated hyper-parameters (the reference's side effect).  Workspace:
+ * bo_compute_mll_workspace_size(n_obj, n).  Synchronous. */
+int bo_optimize_hyperparams_mll(const double* x, int32_t dim, const double* y, int64_t ld_y,
+                                double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
+                                double* prior_variance, double* length_scales, int64_t n, double jitter,
+                                double xtol, double ftol, int64_t maxiter, double min_bound, void* workspace,
+                                size_t workspace_bytes, void* stream, bo_powell_result* res, double* direc);
 
 /* ------------------------------------------------------------------------------------
  * Measurement hooks (bench.py): while enabled, each fused predict kernel launch (the

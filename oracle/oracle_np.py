@@ -74,10 +74,11 @@ def compute_prior_variance(y_vector, n_evaluations, n_objectives):
 
 
 def compute_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance,
-                length_scales, current_eval):
+                length_scales, current_eval, jitter=CHOLESKY_JITTER):
     """bayesopt/numba_kernels.py:152-235 — sum over objectives of the GP marginal log likelihood.
 
     Raises numpy.linalg.LinAlgError when K/pv + 1e-8 I is not positive definite (:214).
+    `jitter`: CHOLESKY_JITTER of the branch (config.py:57-66; 1e-4 in the float32 branch).
     """
     update_k(kernel_matrix, x_vector, 0, current_eval, prior_variance, length_scales)
     n_obj = y_vector.shape[1]
@@ -89,7 +90,7 @@ def compute_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance,
         std = np.std(yc)
         if std > 0.0:
             yc /= std                                                          # (:206-208)
-        l = np.linalg.cholesky(k + CHOLESKY_JITTER * np.eye(n))               # (:211-214)
+        l = np.linalg.cholesky(k + jitter * np.eye(n))                        # (:211-214)
         inter = np.linalg.solve(l, yc)                                         # (:216)
         alpha = np.linalg.solve(l.T, inter)                                    # (:219)
         data_fit = -0.5 * np.dot(yc, alpha)

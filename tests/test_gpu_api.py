@@ -360,7 +360,8 @@ def test_invert_k_lu_path_ill_conditioned(bo):
     res_ref = np.abs(a @ ref - np.eye(n)).max()
     print(f"cond {np.linalg.cond(a):.2e}, residual device {res_got:.3e}, LAPACK {res_ref:.3e}, paths {after}")
     assert res_got <= max(100.0 * res_ref, 1e-6)
-    assert after["lu"] + after["cholesky"] > before["lu"] + before["cholesky"]
+    # LAPACK's Cholesky of this matrix fails; so does the device's: the LU path ran, once
+    assert after["lu"] - before["lu"] == 1 and after["cholesky"] == before["cholesky"]
 
 
 @pytest.mark.parametrize("n,dim,n_obj", [(96, 2, 2), (300, 6, 3)])

@@ -1,20 +1,31 @@
 """BO_PREDICT_FP32 (BASELINE config C5: "fp32 with fp64 reference check"): the f32 matrix-core
 variant of the fused predict + acquisition kernel against the f64 oracle.
 
-Tolerances (written here, SURVEY.md §8c "fp32 (C5)"): variance |d| <= 1e-3 pv; mean
-|d| <= 1e-3 sqrt(pv); the acquisition inherits sqrt(|std var|), whose error near evaluated
-points (std var -> 0) is up to sqrt(1e-3) per objective, so |d acq| <= sum_o (1e-3 + beta_o
-sqrt(1e-3)) pointwise and a median error below 1e-4; selected candidates must be within that
-bound of the reference's best acquisition values."""
+Tolerances (written here; the rule of tests/test_gpu_c5_shards.py): in standardised units the f32
+contraction leaves |d std_mu| <= EPS_MU and |d std_var| <= EPS_VAR; the UCB's square root
+propagates |d sqrt(v)| <= min(sqrt(dv), dv / sqrt(v_ref)), so candidate i's acquisition bound is
+    tol_i = sum_o EPS_MU + beta_o min(sqrt(EPS_VAR), EPS_VAR / sqrt(std_var_ref[o, i]))
+-- ~1e-4 away from the data, ~1e-2 at a training point -- and the selection is judged tie-aware
+on the CPU acquisition array with that per-candidate bound (round 3 allowed 0.19 max|acq| and
+only asked each pick to lie within 2x that of the 16th best)."""
 import numpy as np
 import pytest
 
 from oracle import oracle_np as O
 from fullref import cpu_full
+from parity import check_topq
 
 pytestmark = pytest.mark.gpu
 
-VAR_TOL = 1e-3
+EPS_MU = 1e-5           # |d std_mu|
+EPS_VAR = 1e-5          # |d std_var|
+
+
+def acq_bound(ref_var, pv, betas):
+    """Per-candidate acquisition bound tol_i of the module docstring."""
+    pv, betas = np.asarray(pv)[:, None], np.asarray(betas)[:, None]
+    sv = np.maximum(np.asarray(ref_var) / pv, 1e-300)
+    return np.sum(EPS_MU + betas * np.minimum(np.sqrt(EPS_VAR), EPS_VAR / np.sqrt(sv)), axis=0)
 
 
 @pytest.fixture(scope="module")
@@ -72,21 +83,68 @@ def test_fp32_vs_f64_oracle(bo, n, dim, n_obj, m, ls):
     got = {k: res[k].cpu().numpy() for k in ("mu", "var", "acq", "top_idx")}
     # every candidate against the f64 CPU reference (oracle/cpu_ref.c)
     ref = cpu_full(("fp32", n, dim, m), x, y, cand, kinv, pm, pv, lsv, betas)
-    sq = np.sqrt(pv)[:, None]
-    dv = np.abs(got["var"] - ref["var"]) / pv[:, None]
-    dm = np.abs(got["mu"] - ref["mu"]) / sq
-    assert dv.max() <= VAR_TOL, dv.max()
-    assert dm.max() <= VAR_TOL, dm.max()
-    acq_tol = float(np.sum(1e-3 + betas * np.sqrt(VAR_TOL)))
+    dmu = np.abs(got["mu"] - ref["mu"]) / np.sqrt(pv)[:, None]
+    dvar = np.abs(got["var"] - ref["var"]) / pv[:, None]
+    print(f"fp32 N={n} d={dim}: max |d std_mu| {dmu.max():.3e}, max |d std_var| {dvar.max():.3e}")
+    assert dmu.max() <= EPS_MU, dmu.max()
+    assert dvar.max() <= EPS_VAR, dvar.max()
+    tol = acq_bound(ref["var"], pv, betas)
     da = np.abs(got["acq"] - ref["acq"])
-    assert da.max() <= acq_tol * max(1.0, np.abs(ref["acq"]).max()), da.max()
-    assert np.median(da) <= 1e-4, np.median(da)
-    # selection: 16 distinct, non-evaluated candidates whose reference acquisition is within the
-    # bound of the reference's own best non-evaluated values
-    top = got["top_idx"]
-    assert np.unique(top).size == 16 and (top >= 0).all()
+    bad = da > tol
+    assert not bad.any(), (int(bad.sum()), da[bad][:5], tol[bad][:5])
     xs = {tuple(r) for r in x}
-    assert not any(tuple(cand[i]) in xs for i in top)
-    ref_top = ref["acq"][top]
-    full_ref_best = np.sort(ref["acq"][[tuple(c) not in xs for c in cand]])[::-1][:16]
-    assert ref_top.min() >= full_ref_best[-1] - 2 * acq_tol
+    excl = np.array([tuple(c) in xs for c in cand])
+    check_topq(got["top_idx"], ref["acq"], excl, 16, tol=tol)
+
+
+def test_float32_branch_loop_iteration_c5_shape(bo):
+    """BASELINE C5's shape through the drop-in API in the reference's float32 branch
+    (BayesianOptimization(float_type=np.float32): config.py:54-66 jitters and variance floor,
+    COBYLA for the fit, numba_kernels.py:290-302; the predict on the f32 matrix cores): 2048
+    initial points drawn from the 2^22-point Sobol set, toy_function_3d, one iteration of q = 16.
+    The iteration's acquisition array is checked against the f64 CPU reference computed with the
+    iteration's own fitted hyper-parameters, the float32 branch's jitter (1e-3) and floor (1e-6),
+    on a 2^17-candidate prefix, with the per-candidate bound."""
+    import torch
+    import bench
+    from bayesopt_smart_amd.bayesian_optimization import BayesianOptimization
+    from oracle import cpu_ref
+    cfg = bench.CONFIGS["C5"]
+    cs = bo.CandidateSet.sobol_set(cfg["dim"], cfg["m"], scale=300.0)
+    rng = np.random.default_rng(11)
+    x0 = cs.points(rng.choice(cfg["m"], size=cfg["n_train"], replace=False))
+    f3 = lambda p: bench.toy_function_3d(np.asarray(p, dtype=np.float64)[None])[0]  # noqa: E731
+    seen = []
+    opt = BayesianOptimization(f3, [(0, 300)] * 6, n_objectives=3, n_iterations=1, batch_size=16,
+                               initial_points=x0, input_space=cs, float_type=np.float32,
+                               length_scales=np.full(3, 40.0), betas=np.full(3, 2.0),
+                               callbacks=[lambda st: seen.append({"hyper": np.array(st["hyperparams"]),
+                                                                  "x_next": np.array(st["x_next"]),
+                                                                  "t": dict(st["timings"])})])
+    assert opt.x_vector.dtype == np.float32 and opt.y_vector.dtype == np.float32
+    n = cfg["n_train"]
+    ls0, pm, pv0 = opt.length_scales.astype(np.float64), opt.prior_mean.astype(np.float64), \
+        opt.prior_variance.astype(np.float64)
+    opt.optimize()
+    torch.cuda.synchronize()
+    assert len(seen) == 1 and seen[0]["x_next"].shape == (16, 6)
+    ls, pv = opt.length_scales.astype(np.float64), opt.prior_variance.astype(np.float64)
+    assert not np.array_equal(ls, ls0) or not np.array_equal(pv, pv0)     # the fit ran (COBYLA)
+    print(f"float32 C5-shape iteration: fitted ls {ls}, timings {seen[0]['t']}")
+    x = opt.x_vector[:n].astype(np.float64)
+    y = opt.y_vector[:n].astype(np.float64)
+    km = np.zeros((3, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    kinv = np.stack([np.linalg.inv(km[o] + 1e-3 * np.eye(n)) for o in range(3)])   # KERNEL_JITTER f32
+    m = 1 << 17
+    pts = cs.points(np.arange(m))
+    ref = cpu_ref.predict_acquire(x, y, pts, kinv, pm, pv, ls, opt.betas.astype(np.float64), ucb=True)
+    var = np.maximum(ref["var"], 1e-6)                                        # MIN_VARIANCE f32
+    acq_ref = np.sum((ref["mu"] - pm[:, None]) / np.sqrt(pv)[:, None]
+                     + opt.betas.astype(np.float64)[:, None] * np.sqrt(np.abs(var / pv[:, None])), axis=0)
+    got = opt.acquisition_values[:m]
+    tol = acq_bound(var, pv, opt.betas.astype(np.float64))
+    da = np.abs(got - acq_ref)
+    print(f"max |d acq| {da.max():.3e} (bound at that candidate {tol[np.argmax(da)]:.3e})")
+    bad = da > tol
+    assert not bad.any(), (int(bad.sum()), da[bad][:5], tol[bad][:5])
