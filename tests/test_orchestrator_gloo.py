@@ -91,7 +91,7 @@ class OracleBackend:
         return {"mu_objectives": z, "variance_objectives": z, "acquisition_values": acq}
 
 
-def _run(group=None):
+def _run(group=None, cb_rank0_only=False):
     from bayesopt_smart_amd.bayesian_optimization import optimize
     from bayesopt_smart_amd.predict import CandidateSet
     rng = np.random.default_rng(5)
@@ -111,31 +111,33 @@ def _run(group=None):
         return objective(p)
 
     backend = OracleBackend(cands, group)
+    cb = [lambda st: seen.append(st["acquisition_values"].copy())]
+    if cb_rank0_only and backend.rank != 0:
+        cb = None      # a logging callback on rank 0 only: the gathers must still be collective
     x, y, last = optimize(x, y, None, None, None, None, None, None, None, None, cands, pm, pv,
                           np.zeros(2), N_INIT, T, 2, fn, betas, ls, BATCH, [(0, SIDE), (0, SIDE)],
-                          callbacks=[lambda st: seen.append(st["acquisition_values"].copy())],
-                          backend=backend)
+                          callbacks=cb, backend=backend)
     return x, y, last, ls, seen, len(calls)
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, cb_rank0_only=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        x, y, last, ls, seen, n_calls = _run()
+        x, y, last, ls, seen, n_calls = _run(cb_rank0_only=cb_rank0_only)
         out[rank] = (x.tolist(), y.tolist(), last, ls.tolist(), [a.tolist() for a in seen], n_calls)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_orchestrator_reproduces_single_rank_trajectory(world):
+@pytest.mark.parametrize("world,cb_rank0_only", [(2, False), (3, False), (2, True)])
+def test_gloo_orchestrator_reproduces_single_rank_trajectory(world, cb_rank0_only):
     x1, y1, last1, ls1, seen1, calls1 = _run()
     assert calls1 == T - N_INIT
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, cb_rank0_only), nprocs=world, join=True)
     for r in range(world):
         x, y, last, ls, seen, n_calls = out[r]
         np.testing.assert_array_equal(np.array(x), x1)          # the same batches on every rank
@@ -143,6 +145,9 @@ def test_gloo_orchestrator_reproduces_single_rank_trajectory(world):
         assert last == last1
         np.testing.assert_array_equal(np.array(ls), ls1)
         assert n_calls == (calls1 if r == 0 else 0)             # the objective runs on rank 0 only
+        if cb_rank0_only and r != 0:
+            assert seen == []
+            continue
         assert len(seen) == len(seen1)
         for a, b in zip(seen, seen1):   # gathered shards == the whole array (the oracle's BLAS
             #                             rounds a shard's products at the ulp level differently)
