@@ -64,6 +64,16 @@ class PowellResult(C.Structure):
 
 # int (*)(const double* x, int32_t n, double* f, void* user)
 OBJECTIVE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_double), C.c_void_p)
+# double (*)(double x, int32_t which): tan (0) / atan (1)
+TRIG_FN = C.CFUNCTYPE(C.c_double, C.c_double, C.c_int32)
+
+
+def _numpy_trig(x, which):
+    import numpy
+    return float(numpy.tan(numpy.float64(x)) if which == 0 else numpy.arctan(numpy.float64(x)))
+
+
+NUMPY_TRIG = TRIG_FN(_numpy_trig)    # numpy's tan/atan: scipy's evaluation points bit for bit
 
 
 class SobolDesc(C.Structure):
@@ -113,10 +123,10 @@ _SIGS = {
                                              C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, C.c_double,
                                              c_vp, C.c_size_t, c_vp]),
     "bo_powell_minimize": (C.c_int, [OBJECTIVE_FN, c_vp, c_dbl_p, C.c_int32, c_dbl_p, c_dbl_p, C.c_double,
-                                     C.c_double, C.c_int64, C.c_int64, c_dbl_p, C.POINTER(PowellResult)]),
+                                     C.c_double, C.c_int64, C.c_int64, TRIG_FN, c_dbl_p, C.POINTER(PowellResult)]),
     "bo_optimize_hyperparams_mll": (C.c_int, [c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64, C.c_int32,
                                               c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, C.c_double, C.c_double,
-                                              C.c_double, C.c_int64, C.c_double, c_vp, C.c_size_t, c_vp,
+                                              C.c_double, C.c_int64, C.c_double, TRIG_FN, c_vp, C.c_size_t, c_vp,
                                               C.POINTER(PowellResult), c_dbl_p]),
     "bo_invert_k_path_counts": (C.c_int, [C.POINTER(C.c_int64)]),
     "bo_fit_path_counts": (C.c_int, [C.POINTER(C.c_int64)]),

@@ -825,6 +825,8 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
   const int lr0 = 16 * wave;
   const long long grow0 = wave < 2 ? cK + lr0 : (long long)sb * NB + (lr0 - 32);
   const int ntb = wave == 0 ? 1 : 2;
+  const bool stamp = w == 0 && wave == 0 && o == 0;
+  (void)stamp;
   double av_a[2][4];
 #pragma unroll
   for (int tb = 0; tb < 2; ++tb)
@@ -861,6 +863,7 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
       Cs[(lr0 + li) * CS + t] = av_a[tb][i] - acc[tb][i];
     }
   __syncthreads();
+  if (stamp) FIT_STAMP(3);
   // wave g: columns 8g .. 8g + 7 of every row
   const int c0 = 8 * wave;
   double a[8];
@@ -916,6 +919,7 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
       }
     }
   }
+  if (stamp) FIT_STAMP(4);
   // per-wave partials (own columns), combined through LDS
   double ldp = (lane >= c0 && lane < c0 + 8 && cK + lane < g.n) ? log(dj) : 0.0;
   double zp = 0.0;
@@ -976,6 +980,9 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
       const int np = p_npanel(g, k);
       const int o = (r - T1) / np, w = (r - T1) % np;
       const int sb = k + 1 + w;
+      const bool stamp = w == 0 && o == 0 && wave == 0;
+      (void)stamp;
+      if (stamp) FIT_STAMP(1);
       if (wave == 0) {
         // lanes 0..3: slab k's and slab sb's L column k-1, tiles (k, k) and (sb, k) at version k-1
         bool act = false;
@@ -993,11 +1000,13 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
         if (!ok && lane == 0) *habort = 1;                       // the host reruns the call
       }
       __syncthreads();
+      if (stamp) FIT_STAMP(2);
       if (red[15] != 0.0) {
         p_panel(A + (long long)o * g.ostride, g, o, k, w, part, status, Cs, colb, red);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // every storing wave drains
         __syncthreads();
         if (tid == 0) st_flag(pf_panel(flags, g, o, k, w), 1);
+        if (stamp) FIT_STAMP(5);
       }
       __syncthreads();
       continue;
@@ -1051,6 +1060,9 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
         }
       }
     }
+    const bool tstamp = r == 0 && T1 > 0 && wave == 0;
+    (void)tstamp;
+    if (tstamp) FIT_STAMP(8);
     // this wave's dependencies: L column s of both row blocks, the tile's previous version
     bool ok = true;
     if (have) {
@@ -1066,11 +1078,13 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
         act = true;
       }
       ok = wave_wait(fp, want, act, abort_w);
+      if (tstamp) FIT_STAMP(9);
       if (ok) p_tile_update(A, g, s, tl);
     }
     if (!ok && lane == 0) *habort = 1;                            // the host reruns the call
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // every storing wave drains
     __syncthreads();
+    if (tstamp) FIT_STAMP(10);
     if (have && ok && lane == 0) {
       // the tile's new version (steps applied), stored after the barrier that follows every
       // wave's drain
@@ -1130,11 +1144,23 @@ int fit_factor(double* A, const Geo& g, const double* km, long long ld, const do
 // The persistent path: init launch (which also zeroes the flag words) + ONE fit_persist_kernel
 // launch.  BO_ERR_UNSUPPORTED when the task list exceeds PMAX_STEPS blocks (the caller uses
 // fit_factor).  *habort (host-visible) is set when a wait gave up: the caller reruns fit_factor.
+// the largest column-block count the persistent schedule takes (BO_FIT_PERSIST_MAX_NBT overrides):
+// at N = 2048 (64 blocks) the launch-per-step schedule measured faster (r04c: MLL 0.99 vs 1.06 ms,
+// inverse 1.76 vs 2.38 ms) -- there the trailing update's throughput, not the panel chain, sets
+// the time, and the one-atomic task queue serialises ~13k dequeues
+int persist_max_nbt() {
+  static const int v = [] {
+    const char* e = getenv("BO_FIT_PERSIST_MAX_NBT");
+    return e ? atoi(e) : 48;
+  }();
+  return v;
+}
+
 int fit_factor_persist(double* A, const Geo& g, const double* km, long long ld, const double* x, int dim,
                        const double* y, long long ld_y, const FitParams& p, double* part, int* status,
                        int* flags, int* habort, hipStream_t s) {
   const int steps = g.ident ? g.nbt + 1 : g.nbt;
-  if (steps > PMAX_STEPS) return BO_ERR_UNSUPPORTED;
+  if (steps > PMAX_STEPS || g.nbt > persist_max_nbt()) return BO_ERR_UNSUPPORTED;
   PPlan pl;
   memset(&pl, 0, sizeof(pl));
   pl.steps = steps;

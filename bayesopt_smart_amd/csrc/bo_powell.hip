@@ -5,10 +5,11 @@
 // makes ~200 evaluations), more than the device work the fit needs.  This file restates the
 // algorithm of scipy 1.15 (scipy/optimize/_optimize.py: _minimize_powell, _linesearch_powell,
 // _line_for_search, _minimize_scalar_bounded) operation for operation in IEEE binary64, so that
-// the evaluation sequence, the evaluation count and the result are scipy's.  The one difference:
-// tan/atan come from the C library, numpy's (SIMD) tan differs from it in the last bit for ~0.5 %
-// of arguments, which moves an evaluation point by an ulp (tests/test_powell.py compares the two
-// drivers on the same objectives).
+// the evaluation sequence, the evaluation count and the result are scipy's.  tan/atan (the
+// one-sided line search's transform) come from a caller callback when given -- the Python mirror
+// passes numpy's, which differ from the C library's in the last bit for ~0.5 % of arguments (numpy
+// uses SIMD implementations), so that the evaluation points are scipy's bit for bit -- else from
+// the C library (tests/test_powell.py, tests/test_gpu_fit.py compare the drivers).
 //
 //   bo_powell_minimize             the driver over a caller objective (a C callback)
 //   bo_optimize_hyperparams_mll    the whole fit: Powell over the device MLL terms, memoised per
@@ -36,6 +37,9 @@ struct Fn {
   bo_objective_fn fn;
   void* user;
   int n;
+  bo_trig_fn trig = nullptr;    // tan (which 0) / atan (which 1); NULL = the C library
+  double tan_(double x) const { return trig ? trig(x, 0) : tan(x); }
+  double atan_(double x) const { return trig ? trig(x, 1) : atan(x); }
   long long nfev = 0;
   double maxfun;   // scipy's maxfun (np.inf when only maxiter is given)
   double operator()(const double* x) {
@@ -191,8 +195,9 @@ void linesearch(Fn& func, Vec& p, Vec& xi, double tol, const Vec& lb, const Vec&
     alpha = xs;
   } else {
     // one-sided: the tangent maps (-pi/2, pi/2) onto the line
-    scalar_bounded([&](double t) { return myfunc(tan(t)); }, atan(b0), atan(b1), tol / 100, xs, fs);
-    alpha = tan(xs);
+    scalar_bounded([&](double t) { return myfunc(func.tan_(t)); }, func.atan_(b0), func.atan_(b1), tol / 100, xs,
+                   fs);
+    alpha = func.tan_(xs);
   }
   for (size_t i = 0; i < n; ++i) {
     xi[i] = alpha * xi[i];
@@ -343,7 +348,7 @@ extern "C" {
 
 int bo_powell_minimize(bo_objective_fn fn, void* user, double* x, int32_t n, const double* lb,
                        const double* ub, double xtol, double ftol, int64_t maxiter, int64_t maxfev,
-                       double* direc, bo_powell_result* res) {
+                       bo_trig_fn trig, double* direc, bo_powell_result* res) {
   if (!fn || !x || n < 1 || !lb || !ub || !res) return BO_ERR_ARG;
   memset(res, 0, sizeof(*res));
   // scipy's defaults: maxiter / maxfev None -> N * 1000 each; one given -> the other np.inf
@@ -357,6 +362,7 @@ int bo_powell_minimize(bo_objective_fn fn, void* user, double* x, int32_t n, con
     mf = INFINITY;
   }
   Fn func{fn, user, n};
+  func.trig = trig;
   func.maxfun = mf;
   Vec xv(x, x + n), l(lb, lb + n), u(ub, ub + n);
   std::vector<Vec> dir(n, Vec(n, 0.0));
@@ -373,8 +379,9 @@ int bo_powell_minimize(bo_objective_fn fn, void* user, double* x, int32_t n, con
 int bo_optimize_hyperparams_mll(const double* x, int32_t dim, const double* y, int64_t ld_y,
                                 double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
                                 double* prior_variance, double* length_scales, int64_t n, double jitter,
-                                double xtol, double ftol, int64_t maxiter, double min_bound, void* workspace,
-                                size_t workspace_bytes, void* stream, bo_powell_result* res, double* direc) {
+                                double xtol, double ftol, int64_t maxiter, double min_bound, bo_trig_fn trig,
+                                void* workspace, size_t workspace_bytes, void* stream, bo_powell_result* res,
+                                double* direc) {
   if (!x || !y || !kernel_matrix || !prior_mean || !prior_variance || !length_scales || !res ||
       n_obj < 1 || n_obj > BO_MAX_OBJ || n < 1 || ld < n || dim < 1)
     return BO_ERR_ARG;
@@ -392,7 +399,7 @@ int bo_optimize_hyperparams_mll(const double* x, int32_t dim, const double* y, i
     lb[i] = min_bound;
     ub[i] = INFINITY;
   }
-  int st = bo_powell_minimize(mll_objective, c, x0, np_, lb, ub, xtol, ftol, maxiter, -1, direc, res);
+  int st = bo_powell_minimize(mll_objective, c, x0, np_, lb, ub, xtol, ftol, maxiter, -1, trig, direc, res);
   res->device_calls = c->device_calls;
   // compute_mll's side effect: kernel_matrix holds the Gram of the last evaluated hyper-parameters
   if (c->have_last && (st == BO_OK || st == BO_ERR_NOT_PD)) {

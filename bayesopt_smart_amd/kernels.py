@@ -203,11 +203,12 @@ def _powell_result(x, r, direc):
                           message=_POWELL_MESSAGES.get(int(r.warnflag), ""), x=x)
 
 
-def powell_minimize(fun, x0, bounds, xtol=1e-4, ftol=1e-4, maxiter=None, maxfev=None):
+def powell_minimize(fun, x0, bounds, xtol=1e-4, ftol=1e-4, maxiter=None, maxfev=None, numpy_trig=True):
     """``scipy.optimize.minimize(fun, x0, method="Powell", bounds=bounds, options=...)`` on the
-    library's native driver (bo_powell_minimize: scipy 1.15's algorithm restated in C++; tan/atan
-    from the C library).  `bounds`: sequence of (lo, hi) pairs, None = unbounded.  Returns an
-    OptimizeResult like scipy's; an exception raised by `fun` propagates."""
+    library's native driver (bo_powell_minimize: scipy 1.15's algorithm restated in C++).
+    `numpy_trig`: the one-sided line searches' tan/atan are numpy's (scipy's evaluation points
+    bit for bit), else the C library's.  `bounds`: sequence of (lo, hi) pairs, None = unbounded.
+    Returns an OptimizeResult like scipy's; an exception raised by `fun` propagates."""
     x = np.array(x0, dtype=np.float64).ravel()
     n = x.size
     lb = np.array([-np.inf if b[0] is None else b[0] for b in bounds], dtype=np.float64)
@@ -227,7 +228,8 @@ def powell_minimize(fun, x0, bounds, xtol=1e-4, ftol=1e-4, maxiter=None, maxfev=
     dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
     st = _lib.load().bo_powell_minimize(cfun, None, dp(x), n, dp(lb), dp(ub), float(xtol), float(ftol),
                                         -1 if maxiter is None else int(maxiter),
-                                        -1 if maxfev is None else int(maxfev), dp(direc), C.byref(res))
+                                        -1 if maxfev is None else int(maxfev),
+                                        _lib.NUMPY_TRIG if numpy_trig else _lib.TRIG_FN(), dp(direc), C.byref(res))
     if err:
         raise err[0]
     _lib.check(st, "bo_powell_minimize")
@@ -235,15 +237,18 @@ def powell_minimize(fun, x0, bounds, xtol=1e-4, ftol=1e-4, maxiter=None, maxfev=
 
 
 def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prior_variance,
-                             length_scales, current_eval, memo=True, *, float_type=None, driver="native"):
+                             length_scales, current_eval, memo=True, *, float_type=None, driver="native",
+                             numpy_trig=True):
     """numba_kernels.py:238-321 — maximise the device MLL over [ls..., var...] (bounds >= 1e-5);
     updates length_scales and prior_variance in place, returns the OptimizeResult.  The training
     arrays are staged on the device once for all ~100-300 MLL evaluations.
 
     float64 (the reference's default branch): Powell (:305-315).  driver "native" (default) runs
     the whole fit as ONE library call, bo_optimize_hyperparams_mll: the Powell driver in C++ around
-    the device MLL, no Python per evaluation; driver "scipy" runs scipy's Powell over the same
-    device terms (the pre-round-4 path, kept for comparison).  float32 (:290-302): scipy's COBYLA
+    the device MLL, no Python per evaluation except numpy's tan/atan for the one-sided line
+    searches (`numpy_trig`, so that the evaluation points are scipy's bit for bit; False: the C
+    library's, no Python at all); driver "scipy" runs scipy's Powell over the same device terms
+    (the pre-round-4 path, kept for comparison).  float32 (:290-302): scipy's COBYLA
     with rhobeg 1.0 and tol 10 ftol over the MLL with the float32 jitter.
 
     `memo`: the MLL is a sum of per-objective terms, each a function of (x, y, pm, ls_o) only --
@@ -279,7 +284,8 @@ def optimize_hyperparams_mll(x_vector, y_vector, kernel_matrix, prior_mean, prio
         st = lib.bo_optimize_hyperparams_mll(
             xd.data_ptr(), xd.shape[1], yd.data_ptr(), yd.stride(0), km.ptr, km.t.shape[-1], n_obj, dp(pm_c),
             dp(pv_io), dp(ls_io), n, chol_jitter, HYPERPARAM_XTOL, HYPERPARAM_FTOL, HYPERPARAM_MAXITER,
-            HYPERPARAM_MIN_BOUND, ws.data_ptr(), ws.numel(), stream_handle(dev), C.byref(res), dp(direc))
+            HYPERPARAM_MIN_BOUND, _lib.NUMPY_TRIG if numpy_trig else _lib.TRIG_FN(), ws.data_ptr(), ws.numel(),
+            stream_handle(dev), C.byref(res), dp(direc))
         if st != _lib.ERR_UNSUPPORTED:
             km.finish()
             _lib.check(st, "bo_optimize_hyperparams_mll")

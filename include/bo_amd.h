@@ -312,6 +312,10 @@ size_t bo_compute_mll_workspace_size(int32_t n_obj, int64_t n);
  * ---------------------------------------------------------------------------------- */
 /* objective: *f = f(x[0..n)); a non-zero return aborts the minimisation with that status */
 typedef int (*bo_objective_fn)(const double* x, int32_t n, double* f, void* user);
+/* tan (which = 0) / atan (which = 1) of the one-sided line searches' transform; NULL = the C
+ * library's.  A caller wanting scipy's evaluation points bit for bit passes numpy's (its SIMD
+ * tan differs from the C library's in the last bit for ~0.5 % of arguments). */
+typedef double (*bo_trig_fn)(double x, int32_t which);
 typedef struct bo_powell_result {
   double fun;             /* final objective value                                          */
   int64_t nfev;           /* objective evaluations                                          */
@@ -326,7 +330,7 @@ typedef struct bo_powell_result {
  * (scipy's bracketing Brent; the fit's bounds never need it). */
 int bo_powell_minimize(bo_objective_fn fn, void* user, double* x, int32_t n, const double* lb,
                        const double* ub, double xtol, double ftol, int64_t maxiter, int64_t maxfev,
-                       double* direc, bo_powell_result* res);
+                       bo_trig_fn trig, double* direc, bo_powell_result* res);
 /* optimize_hyperparams_mll (numba_kernels.py:238-321) as ONE call: Powell over [ls..., pv...] from
  * the given values (host, updated in place on success), bounds [min_bound, inf), maximising the
  * device MLL (bo_compute_mll_each_jitter; each per-objective term memoised per distinct ls_o, a
@@ -336,8 +340,9 @@ int bo_powell_minimize(bo_objective_fn fn, void* user, double* x, int32_t n, con
 int bo_optimize_hyperparams_mll(const double* x, int32_t dim, const double* y, int64_t ld_y,
                                 double* kernel_matrix, int64_t ld, int32_t n_obj, const double* prior_mean,
                                 double* prior_variance, double* length_scales, int64_t n, double jitter,
-                                double xtol, double ftol, int64_t maxiter, double min_bound, void* workspace,
-                                size_t workspace_bytes, void* stream, bo_powell_result* res, double* direc);
+                                double xtol, double ftol, int64_t maxiter, double min_bound, bo_trig_fn trig,
+                                void* workspace, size_t workspace_bytes, void* stream, bo_powell_result* res,
+                                double* direc);
 
 /* ------------------------------------------------------------------------------------
  * Measurement hooks (bench.py): while enabled, each fused predict kernel launch (the

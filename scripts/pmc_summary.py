@@ -43,10 +43,13 @@ def main(src, dst, workload="C3", alg_bytes=40 * 1048576, kernel_label="cm_predi
         write = mean["WRITE_SIZE"] * 1024.0
         out.update({"fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
                     "hbm_bytes_per_launch": fetch + write,
-                    "algorithmic_bytes_per_launch": alg_bytes,
-                    "traffic_ratio": (fetch + write) / alg_bytes,
                     "note": "FETCH_SIZE x2 (gfx950 16-B streaming-read correction), KiB -> B; "
                             "algorithmic = outputs written (+ explicit coordinates read)"})
+        if alg_bytes and alg_bytes > 1.0:   # no ratio without a real algorithmic byte count
+            out.update({"algorithmic_bytes_per_launch": alg_bytes,
+                        "traffic_ratio": (fetch + write) / alg_bytes})
+        if os.environ.get("PMC_ALG_NOTE"):
+            out["algorithmic_bytes_basis"] = os.environ["PMC_ALG_NOTE"]
     if "SQ_INSTS_MFMA" in mean and "SQ_INSTS_VALU" in mean:
         out["valu_per_mfma"] = mean["SQ_INSTS_VALU"] / max(mean["SQ_INSTS_MFMA"], 1.0)
         # SQ_INSTS_VALU counts the MFMAs too (C4: 2.7 per MFMA against ~1.7 other VALU per MFMA
@@ -61,4 +64,4 @@ def main(src, dst, workload="C3", alg_bytes=40 * 1048576, kernel_label="cm_predi
 
 if __name__ == "__main__":
     a = sys.argv[1:]
-    main(a[0], a[1], *([a[2], float(a[3])] + a[4:5] if len(a) > 2 else []))
+    main(a[0], a[1], *([a[2], (None if a[3] == "none" else float(a[3]))] + a[4:5] if len(a) > 2 else []))
