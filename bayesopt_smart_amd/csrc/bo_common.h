@@ -440,11 +440,12 @@ static __global__ __launch_bounds__(256) void bo_topq_merge_kernel(const TopEntr
   }
 }
 
-// invert_k's blocked LU path (bo_lu.hip), called by bo_invert_k (bo_fit.hip) per objective
-size_t bo_lu_workspace_size(int64_t n);
+// invert_k's blocked LU path (bo_lu.hip), called by bo_invert_k (bo_fit.hip) once for all the
+// objectives whose Cholesky failed (out[b] / km[b], b < n_lu)
+size_t bo_lu_workspace_size(int64_t n, int n_lu);
 int bo_lu_max_n();
-int bo_lu_inverse(double* out, const double* km, int64_t ld, int64_t n, double jitter, void* ws,
-                  size_t ws_bytes, hipStream_t s);
+int bo_lu_inverse(double* const* out, const double* const* km, int n_lu, int64_t ld, int64_t n, double jitter,
+                  void* ws, size_t ws_bytes, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------
 // Sobol candidates (BO_CAND_SOBOL): direction numbers (host) and one coordinate (device).

@@ -934,17 +934,23 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
     red[8 + wave] = bad ? 1.0 : 0.0;
   }
   __syncthreads();
-  if (tid == 0) {
-    const bool any_bad = red[8] + red[9] + red[10] + red[11] != 0.0;
-    if (g.ident) {
-      if (w == 0 && any_bad) atomicOr(status + o, 1);
-    } else {
-      if (w == 0) {
-        part[(long long)o * part_len(g) + k] = ((red[0] + red[1]) + red[2]) + red[3];
-        if (any_bad) status[o] = 1;
-      }
-      if (sb == g.nbt) part[(long long)o * part_len(g) + g.nbt + k] = ((red[4] + red[5]) + red[6]) + red[7];
+}
+
+// The panel's partials and status (thread 0), stored AFTER its completion flag: for the MLL they
+// go to pinned host memory, and a drain behind such a store (~3 us, phase stamps) would sit on
+// the critical path of the next panel.
+__device__ __forceinline__ void p_panel_partials(const Geo& g, int o, int k, int w, double* __restrict__ part,
+                                                 int* __restrict__ status, const double* red) {
+  const int sb = k + 1 + w;
+  const bool any_bad = red[8] + red[9] + red[10] + red[11] != 0.0;
+  if (g.ident) {
+    if (w == 0 && any_bad) atomicOr(status + o, 1);
+  } else {
+    if (w == 0) {
+      part[(long long)o * part_len(g) + k] = ((red[0] + red[1]) + red[2]) + red[3];
+      if (any_bad) status[o] = 1;
     }
+    if (sb == g.nbt) part[(long long)o * part_len(g) + g.nbt + k] = ((red[4] + red[5]) + red[6]) + red[7];
   }
 }
 
@@ -1005,7 +1011,10 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
         p_panel(A + (long long)o * g.ostride, g, o, k, w, part, status, Cs, colb, red);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // every storing wave drains
         __syncthreads();
-        if (tid == 0) st_flag(pf_panel(flags, g, o, k, w), 1);
+        if (tid == 0) {
+          st_flag(pf_panel(flags, g, o, k, w), 1);
+          p_panel_partials(g, o, k, w, part, status, red);
+        }
         if (stamp) FIT_STAMP(5);
       }
       __syncthreads();
@@ -1295,17 +1304,24 @@ int bo_invert_k_jitter(double* out, const double* km, int64_t ld, int32_t n_obj,
     if (!fail[o]) __atomic_fetch_add(&g_inv_paths[0], 1, __ATOMIC_RELAXED);
   }
   // LU path for the objectives whose Cholesky failed or whose K is not symmetric: the blocked
-  // LU with partial pivoting of bo_lu.hip in the (now free) augmented-matrix region; Gauss-Jordan
-  // with partial pivoting above its register capacity (N > 2048)
+  // LU with partial pivoting of bo_lu.hip, all of them in one launch sequence, in the (now free)
+  // augmented-matrix region; Gauss-Jordan with partial pivoting above its register capacity
+  // (N > 2048)
+  {
+    double* lu_out[BO_MAX_OBJ];
+    const double* lu_km[BO_MAX_OBJ];
+    int n_lu = 0;
+    for (int o = 0; o < n_obj; ++o)
+      if (fail[o]) { lu_out[n_lu] = out + (long long)o * n * n; lu_km[n_lu] = km + (long long)o * ld * ld; ++n_lu; }
+    if (n_lu > 0 && n <= bo_lu_max_n() && geo_bytes(g) >= bo_lu_workspace_size(n, n_lu)) {
+      const int st2 = bo_lu_inverse(lu_out, lu_km, n_lu, ld, n, jitter, A, geo_bytes(g), s);
+      __atomic_fetch_add(&g_inv_paths[1], n_lu, __ATOMIC_RELAXED);
+      if (st2 != BO_OK) return st2;
+      for (int o = 0; o < n_obj; ++o) fail[o] = 0;
+    }
+  }
   for (int o = 0; o < n_obj; ++o) {
     if (!fail[o]) continue;
-    if (n <= bo_lu_max_n() && geo_bytes(g) >= bo_lu_workspace_size(n)) {
-      const double* ko = km + (long long)o * ld * ld;
-      const int st2 = bo_lu_inverse(out + (long long)o * n * n, ko, ld, n, jitter, A, geo_bytes(g), s);
-      __atomic_fetch_add(&g_inv_paths[1], 1, __ATOMIC_RELAXED);
-      if (st2 != BO_OK) return st2;
-      continue;
-    }
     __atomic_fetch_add(&g_inv_paths[2], 1, __ATOMIC_RELAXED);
     int* gstat = status + BO_MAX_OBJ + 1;
     BO_CHECK_HIP(hipMemsetAsync(gstat, 0, sizeof(int), s));
@@ -1353,6 +1369,23 @@ int bo_invert_k_path_counts(int64_t* counts) {
   for (int i = 0; i < 3; ++i) counts[i] = __atomic_load_n(&g_inv_paths[i], __ATOMIC_RELAXED);
   return BO_OK;
 }
+
+#ifdef BO_FIT_TIMING
+// diagnostic build only: copy the phase stamps of the calls since the last read (pairs of
+// [tag word, 100 MHz clock]) to `out` (host, 2 cap words) and reset the count; returns the count
+__attribute__((visibility("default"))) int bo_debug_fit_timing(long long* out, int cap) {
+  int cnt = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(bo_fit_tcount), sizeof(int)) != hipSuccess) return -1;
+  if (cnt > cap) cnt = cap;
+  if (cnt > 4096) cnt = 4096;
+  if (cnt > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_fit_tstamp), sizeof(long long) * 2 * cnt) != hipSuccess)
+    return -1;
+  const int zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(bo_fit_tcount), &zero, sizeof(int)) != hipSuccess) return -1;
+  return cnt;
+}
+#endif
 
 int bo_fit_path_counts(int64_t* counts) {
   if (!counts) return BO_ERR_ARG;

@@ -2,26 +2,35 @@
 // right-looking LU with partial pivoting (getrf's pivot: the first row of largest |a_ij| in
 // the column, rows >= j), then inv(A) = U^-1 L^-1 P one 16-column strip of the identity at a
 // time (getrs).  Taken by bo_invert_k for the objectives whose Cholesky fails (cond(K + 1e-6 I)
-// of 1e14..1e18 with Powell-fitted hyper-parameters) or whose K is not symmetric.
+// of 1e14..1e18 with Powell-fitted hyper-parameters) or whose K is not symmetric;
+// every such objective of one call is factored in the same launches (grid y = the objective).
 //
 // A (N padded to 16 with identity) is column-major in the workspace.  A 16-column STRIP's rows
 // are held up to four per thread of a 512-thread workgroup (16 doubles per row in registers).
 // Launch k (one per 16-column step):
-//   * panel (strip k): applies the pending step k-1 to its strip -- the step's 16 row swaps (as
-//     one permutation of <= 32 rows through LDS), U12 = L11^-1 A12 (unit lower 16 x 16) and the
-//     rank-16 update of the rows below -- then factors the strip: per column a workgroup argmax
-//     (wave shuffles + 16 wave results in LDS), the row swap through LDS, the scaled column and
-//     the rank-1 update of the strip's remaining columns;
+//   * panel (strip k): applies the pending step k-1 to its strip -- the step's row permutation
+//     (<= 32 rows through LDS), U12 = L11^-1 A12 (16 lanes, each column's substitution chain in
+//     registers) and the rank-16 update of the rows below -- then factors the strip.  Per column
+//     ONE barrier: every wave publishes its best row (value, index and the row's 16 entries: wave
+//     max by shuffles, the lowest row among the lanes holding it by ballots) and the thread holding
+//     row j publishes that row, into a buffer alternating by column parity; after the barrier every
+//     thread picks the pivot among the 8 wave results, swaps and applies the rank-1 update to its
+//     own rows.  Wave 0 then composes the step's 16 swaps into one permutation record (pos <- src
+//     pairs, by ballots over 32 lanes) that every later consumer reads;
 //   * update (strips > k): step k-1 applied to each strip by its own workgroup (lookahead: the
 //     panel of step k needs only its own strip).
 // The L columns keep the row order of their own step (later swaps are not applied to them:
 // LAPACK's laswp on the left columns), so the solve interleaves the swaps with the forward
 // substitution exactly as the elimination applied them.  Solve (one launch, one workgroup per
-// strip of the identity, no inter-workgroup dependency): W = e_strip; per step s: the 16 swaps,
-// W_s = L11^-1 W_s, W_below -= L21 W_s; then per step from the last: W_s = U_ss^-1 W_s,
-// W_above -= U_above,s W_s.  W's rows are out[:, strip].
+// strip of the identity and objective, no inter-workgroup dependency): W = e_strip; per step s:
+// the step's permutation record (prefetched one step ahead), W_s = L11^-1 W_s, W_below -= L21 W_s;
+// then per step from the last: W_s = U_ss^-1 W_s, W_above -= U_above,s W_s.  W's rows are
+// out[:, strip].
 //
-// Round 2 ran one Gauss-Jordan launch per pivot (N launches, ~105 ms at N = 2048).
+// Round 2 ran one Gauss-Jordan launch per pivot (N launches, ~105 ms at N = 2048); round 3's
+// version of this file (one objective per launch sequence, the permutation rebuilt serially by
+// one thread in every consumer, two barriers per pivot column) took 3.2 ms per objective at
+// N = 512.
 
 #include "bo_common.h"
 
@@ -34,19 +43,59 @@ namespace {
 
 constexpr int LB = 16;          // strip width
 constexpr int LT = 512;         // threads per strip workgroup (256 VGPRs: the rows stay in registers)
-constexpr int LR = 4;           // rows per thread: N_p <= LT * LR = 2048
+constexpr int LRMAX = 4;        // rows per thread (kernels templated on LR = 1, 2, 4 by N_p): N_p <= 2048
+constexpr int LW = LT / 64;     // waves per workgroup
+constexpr int PREC = 72;        // ints per step's permutation record: [0] m, [8, 40) pos, [40, 72) src
+
+// Diagnostic build (BO_BUILD_VARIANT=DEF_FIT_TIMING): the panel workgroup of each step launch
+// and workgroup 0 of the solve stamp the 100 MHz real-time clock at their phase boundaries
+// (word: step << 16 | slot << 4 | tag); bo_debug_lu_timing reads them back.
+#define LB_DIAG 16
+#ifdef BO_FIT_TIMING
+__device__ long long bo_lu_tstamp[8192];
+__device__ int bo_lu_tcount;
+#define LU_STAMP(step, tag)                                                          \
+  do {                                                                               \
+    if (threadIdx.x == 0) {                                                          \
+      const int _i = atomicAdd(&bo_lu_tcount, 1);                                    \
+      if (_i < 4096) {                                                               \
+        bo_lu_tstamp[2 * _i] = ((long long)(step) << 16) | ((long long)blockIdx.y << 4) | (tag); \
+        bo_lu_tstamp[2 * _i + 1] = (long long)wall_clock64();                        \
+      }                                                                              \
+    }                                                                                \
+  } while (0)
+// per pivot column of the panel (slot 0, steps < 64): plain stores of the clock, no atomics
+__device__ long long bo_lu_cstamp[64 * LB_DIAG * 4];
+#define LU_CSTAMP(step, j, t)                                                        \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.y == 0 && (step) < 64)                          \
+      bo_lu_cstamp[((step) * LB_DIAG + (j)) * 4 + (t)] = (long long)wall_clock64();  \
+  } while (0)
+#else
+#define LU_STAMP(step, tag) ((void)0)
+#define LU_CSTAMP(step, j, t) ((void)0)
+#endif
 
 struct LuGeo {
   int n, n_p, nbs;              // N, N padded to 16, strips
   long long Na;                 // leading dimension (= n_p)
 };
 
+struct LuBatch {                // one factorisation per slot (the objectives whose Cholesky failed)
+  double* A[BO_MAX_OBJ];
+  int* prec[BO_MAX_OBJ];        // nbs permutation records
+  const double* km[BO_MAX_OBJ];
+  double* out[BO_MAX_OBJ];
+  int* status;                  // [slot]: 1 = an exactly zero (or NaN) pivot
+};
+
 // ------------------------------------------------------------------------------ init
-// A(i, j) = K[i][j] + 1e-6 d_ij (i, j < N), identity padding: 32 x 32 tiles, coalesced both ways
-__global__ __launch_bounds__(256) void lu_init_kernel(double* __restrict__ A, LuGeo g,
-                                                      const double* __restrict__ km, long long ld, double jitter) {
+// A(i, j) = K[i][j] + jitter d_ij (i, j < N), identity padding: 32 x 32 tiles, coalesced both ways
+__global__ __launch_bounds__(256) void lu_init_kernel(LuBatch bt, LuGeo g, long long ld, double jitter) {
   __shared__ double tile[32][33];
   const int ti = blockIdx.y, tj = blockIdx.x, tid = threadIdx.x;
+  const double* __restrict__ km = bt.km[blockIdx.z];
+  double* __restrict__ A = bt.A[blockIdx.z];
   for (int e = tid; e < 32 * 32; e += 256) {
     const int rr = e >> 5, cc = e & 31;               // K row-major: consecutive threads -> columns
     const long long i = (long long)ti * 32 + rr, j = (long long)tj * 32 + cc;
@@ -64,192 +113,386 @@ __global__ __launch_bounds__(256) void lu_init_kernel(double* __restrict__ A, Lu
 
 // --------------------------------------------------------------------- strip helpers
 struct StripLds {
-  double buf[32][LB];           // swapped rows in flight
+  double buf[32][LB];           // permuted rows in flight
   int pos[32], src[32];         // the step's row permutation: pos <- src
-  int trow[32], tsrc[32];       // thread 0's scratch while building it
   int m;                        // its length
   double T[LB][LB + 1];         // the 16 x 16 block being solved
   double L11[LB][LB + 1];       // the step's diagonal block (L unit lower / U upper)
-  double redv[LT / 64];
-  int redi[LT / 64];
-  double prow[LB], grow[LB];    // pivot row / displaced row
-  int pivot;
-  double pivv;
+  double cand[2][LW][LB];       // panel: each wave's best row, by column parity
+  unsigned long long ck[2][LW]; //        its pivot key
+  int cr[2][LW];                //        its row index
+  double grow[2][LB];           //        row j of the column
+  int piv[LB];                  //        the step's pivot rows
+  short smap[LT * LRMAX];          // row -> its slot as a source of the permutation (-1: none)
+  short pmap[LT * LRMAX];          // row -> its slot as a destination
 };
+
+__device__ __forceinline__ void init_maps(StripLds& L) {
+  for (int i = threadIdx.x; i < LT * LRMAX; i += LT) { L.smap[i] = -1; L.pmap[i] = -1; }
+}
 
 // row `base + t + LT r` of the strip is w[r][*] of thread t
 __device__ __forceinline__ long long own_row(int base, int r) { return (long long)base + threadIdx.x + (long long)LT * r; }
 
-// The row permutation of step s's 16 swaps (rows 16 s + j <-> ipiv[16 s + j], in order), as
-// pos <- src pairs over the <= 32 rows it moves; built by thread 0.
-__device__ void step_perm(StripLds& L, const int* __restrict__ ipiv, int s) {
-  if (threadIdx.x == 0) {
-    int* rows = L.trow;
-    int* src = L.tsrc;
-    int m = 0;
-    for (int j = 0; j < LB; ++j) {
-      const int a = LB * s + j, b = ipiv[LB * s + j];
-      int ia = -1, ib = -1;
-      for (int u = 0; u < m; ++u) { if (rows[u] == a) ia = u; if (rows[u] == b) ib = u; }
-      if (ia < 0) { rows[m] = a; src[m] = a; ia = m++; }
-      if (ib < 0) { rows[m] = b; src[m] = b; ib = m++; }
-      const int t = src[ia]; src[ia] = src[ib]; src[ib] = t;
-    }
-    int k = 0;
-    for (int u = 0; u < m; ++u)
-      if (src[u] != rows[u]) { L.pos[k] = rows[u]; L.src[k] = src[u]; ++k; }
-    L.m = k;
-  }
-  __syncthreads();
+// the permutation record's pairs into LDS (threads 0..31 hold them in registers, loaded earlier),
+// and the row -> slot maps
+__device__ __forceinline__ void put_perm(StripLds& L, int m, int pos, int src) {
+  if (threadIdx.x < 32) { L.pos[threadIdx.x] = pos; L.src[threadIdx.x] = src; }
+  if ((int)threadIdx.x < m) { L.smap[src] = (short)threadIdx.x; L.pmap[pos] = (short)threadIdx.x; }
+  if (threadIdx.x == 0) L.m = m;
 }
 
-// apply the permutation to the rows held in registers (rows >= base)
-__device__ __forceinline__ void apply_perm(StripLds& L, double (&w)[LR][LB], int base) {
+__device__ __forceinline__ void get_perm(const int* __restrict__ rec, int& m, int& pos, int& src) {
+  const int t = threadIdx.x & 31;
+  m = rec[0];
+  pos = rec[8 + t];
+  src = rec[40 + t];
+}
+
+// apply the permutation in LDS to the rows held in registers (rows >= base); the caller has
+// synchronised after put_perm.  One map lookup per row (a scan over the <= 32 slots per row, with
+// its dependent LDS reads, cost ~5 us per call).
+template <int LR>
+__device__ __forceinline__ void apply_perm(StripLds& L, double (&w)[LR][LB], int base, int n_p) {
   const int m = L.m;
+  if (m == 0) return;                                 // uniform
 #pragma unroll
   for (int r = 0; r < LR; ++r) {
     const long long row = own_row(base, r);
-    for (int u = 0; u < m; ++u)
-      if (L.src[u] == row) {
+    const int u = row < n_p ? L.smap[row] : -1;
+    if (u >= 0) {
 #pragma unroll
-        for (int c = 0; c < LB; ++c) L.buf[u][c] = w[r][c];
-      }
+      for (int c = 0; c < LB; ++c) L.buf[u][c] = w[r][c];
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < LR; ++r) {
     const long long row = own_row(base, r);
-    for (int u = 0; u < m; ++u)
-      if (L.pos[u] == row) {
+    const int u = row < n_p ? L.pmap[row] : -1;
+    if (u >= 0) {
 #pragma unroll
-        for (int c = 0; c < LB; ++c) w[r][c] = L.buf[u][c];
-      }
+      for (int c = 0; c < LB; ++c) w[r][c] = L.buf[u][c];
+    }
   }
   __syncthreads();
+  if ((int)threadIdx.x < m) { L.smap[L.src[threadIdx.x]] = -1; L.pmap[L.pos[threadIdx.x]] = -1; }
 }
 
-// Step s applied to a strip whose rows [16 s, n_p) are in registers (base = 16 s): swaps,
-// U12 = L11^-1 A12 (rows 16 s .. 16 s + 15), A22 -= L21 U12.
-__device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const int* __restrict__ ipiv, int s,
+// Pivot search key of an entry: 0 for a row outside the column (or NaN: idamax skips it),
+// else the bits of |a| + 1 (monotone in |a| for non-negative doubles).  Ties go to the lower row.
+__device__ __forceinline__ unsigned long long piv_key(double a, bool in) {
+  const double v = fabs(a);
+  return (in && v == v) ? (unsigned long long)__double_as_longlong(v) + 1ull : 0ull;
+}
+__device__ __forceinline__ bool piv_before(unsigned long long ka, int ra, unsigned long long kb, int rb) {
+  return ka > kb || (ka == kb && ra < rb);
+}
+template <int CTRL>
+__device__ __forceinline__ void piv_dpp_step(unsigned long long& k, int& r) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)k, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(k >> 32), CTRL, 0xF, 0xF, false);
+  const int orr = __builtin_amdgcn_update_dpp(0, r, CTRL, 0xF, 0xF, false);
+  const unsigned long long ok = ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
+  const bool t = piv_before(ok, orr, k, r);
+  k = t ? ok : k;
+  r = t ? orr : r;
+}
+// the wave's best (key, row), wave-uniform: quad_perm xor 1 and xor 2, row_half_mirror,
+// row_mirror (each 16-lane row then holds its best), then the 4 row bests by v_readlane
+__device__ __forceinline__ void piv_wave_best(unsigned long long k, int r, unsigned long long& wk, int& wr) {
+  piv_dpp_step<0xB1>(k, r);
+  piv_dpp_step<0x4E>(k, r);
+  piv_dpp_step<0x141>(k, r);
+  piv_dpp_step<0x140>(k, r);
+  wk = bo_readlane_u(k, 0);
+  wr = __builtin_amdgcn_readlane(r, 0);
+#pragma unroll
+  for (int l = 16; l < 64; l += 16) {
+    const unsigned long long rk = bo_readlane_u(k, l);
+    const int rr = __builtin_amdgcn_readlane(r, l);
+    const bool t = piv_before(rk, rr, wk, wr);
+    wk = t ? rk : wk;
+    wr = t ? rr : wr;
+  }
+}
+
+// Wave 0: the 16 swaps (rows 16 s + j <-> piv[j], in order) composed into pos <- src pairs over
+// the <= 32 rows they move; lane u holds slot u (its row, and which row's data ends there).
+__device__ void build_perm(const StripLds& L, int s, int* __restrict__ rec) {
+  const int lane = threadIdx.x & 63;
+  const int pivl = L.piv[lane & (LB - 1)];             // lane j holds pivot j
+  int myrow = -1, mysrc = -1, m = 0;
+#pragma unroll 1
+  for (int j = 0; j < LB; ++j) {
+    const int a = LB * s + j, b = __builtin_amdgcn_readlane(pivl, j);
+    if (a == b) continue;
+    const unsigned long long ma = __ballot(myrow == a);
+    int ia = m;
+    if (ma) ia = __builtin_ctzll(ma);
+    else { if (lane == m) { myrow = a; mysrc = a; } ++m; }
+    const unsigned long long mb = __ballot(myrow == b);
+    int ib = m;
+    if (mb) ib = __builtin_ctzll(mb);
+    else { if (lane == m) { myrow = b; mysrc = b; } ++m; }
+    const int sa = __builtin_amdgcn_readlane(mysrc, ia), sb = __builtin_amdgcn_readlane(mysrc, ib);
+    if (lane == ia) mysrc = sb;
+    if (lane == ib) mysrc = sa;
+  }
+  const bool moved = lane < m && mysrc != myrow;
+  const unsigned long long mk = __ballot(moved);
+  const int k = __popcll(mk & ((1ull << lane) - 1ull));
+  if (moved) { rec[8 + k] = myrow; rec[40 + k] = mysrc; }
+  if (lane == 0) rec[0] = __popcll(mk);
+}
+
+// L.T = L11^-1 L.T (unit lower), one column per lane 0..15, the chain in registers
+__device__ __forceinline__ void trsm_lower(StripLds& L) {
+  const int t = threadIdx.x;
+  if (t < LB) {
+    double x[LB];
+#pragma unroll
+    for (int i = 0; i < LB; ++i) x[i] = L.T[i][t];
+#pragma unroll
+    for (int i = 1; i < LB; ++i)
+#pragma unroll
+      for (int m2 = 0; m2 < i; ++m2) x[i] = __builtin_fma(-L.L11[i][m2], x[m2], x[i]);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) L.T[i][t] = x[i];
+  }
+}
+
+// L.T = U^-1 L.T (upper with its diagonal)
+__device__ __forceinline__ void trsm_upper(StripLds& L) {
+  const int t = threadIdx.x;
+  if (t < LB) {
+    double x[LB];
+#pragma unroll
+    for (int i = 0; i < LB; ++i) x[i] = L.T[i][t];
+#pragma unroll
+    for (int i = LB - 1; i >= 0; --i) {
+#pragma unroll
+      for (int m2 = i + 1; m2 < LB; ++m2) x[i] = __builtin_fma(-L.L11[i][m2], x[m2], x[i]);
+      x[i] = x[i] / L.L11[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) L.T[i][t] = x[i];
+  }
+}
+
+// w[r] -= sum_m2 A(b + m2 column, row_r) T[m2][*] on the rows with act[r]: a rolled loop over
+// groups of 4 columns with the next group's column values in flight (the fully unrolled form,
+// 1024 FMAs with their loads, was ~10 KB of code per copy run once per launch).  r16_start issues
+// the first group's loads, early (before the barriers that precede the update).
+template <int LR>
+struct R16 {
+  long long ra[LR];             // the row each lane loads (inactive rows: row b, never used)
+  double lq[4][LR];
+};
+
+template <int LR>
+__device__ __forceinline__ void r16_start(const double* __restrict__ A, long long Na, int b, int base,
+                                          const bool (&act)[LR], R16<LR>& st) {
+#pragma unroll
+  for (int r = 0; r < LR; ++r) st.ra[r] = act[r] ? own_row(base, r) : b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < LR; ++r) st.lq[q][r] = A[(long long)(b + q) * Na + st.ra[r]];
+}
+
+template <int LR>
+__device__ __forceinline__ void r16_finish(const double* __restrict__ A, long long Na, int b, const StripLds& L,
+                                           double (&w)[LR][LB], const bool (&act)[LR], R16<LR>& st) {
+#pragma unroll 1
+  for (int m0 = 0; m0 < LB; m0 += 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double lc[LR];
+#pragma unroll
+      for (int r = 0; r < LR; ++r) lc[r] = st.lq[q][r];
+      if (m0 + 4 < LB) {
+#pragma unroll
+        for (int r = 0; r < LR; ++r) st.lq[q][r] = A[(long long)(b + m0 + 4 + q) * Na + st.ra[r]];
+      }
+      double t[LB];
+#pragma unroll
+      for (int c = 0; c < LB; ++c) t[c] = L.T[m0 + q][c];
+#pragma unroll
+      for (int r = 0; r < LR; ++r)
+        if (act[r]) {
+#pragma unroll
+          for (int c = 0; c < LB; ++c) w[r][c] = __builtin_fma(-lc[r], t[c], w[r][c]);
+        }
+    }
+  }
+}
+
+// Step s applied to a strip whose rows [16 s, n_p) are in registers (base = 16 s): the
+// permutation, U12 = L11^-1 A12 (rows 16 s .. 16 s + 15), A22 -= L21 U12.
+template <int LR>
+__device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const int* __restrict__ rec, int s,
                             StripLds& L, double (&w)[LR][LB]) {
   const int base = LB * s, tid = threadIdx.x;
-  step_perm(L, ipiv, s);
-  apply_perm(L, w, base);
+  // every global load of the step issued first: the permutation record, L11, the first columns
+  // of L21
+  int pm = 0, pp = 0, ps = 0;
+  if (tid < 32) get_perm(rec, pm, pp, ps);
+  const double l11 = tid < LB * LB ? A[(long long)(base + (tid >> 4)) * g.Na + base + (tid & 15)] : 0.0;
+  bool act[LR];
+#pragma unroll
+  for (int r = 0; r < LR; ++r) act[r] = own_row(base, r) >= base + LB && own_row(base, r) < g.n_p;
+  R16<LR> st;
+  r16_start(A, g.Na, base, base, act, st);
+  put_perm(L, pm, pp, ps);
+  __syncthreads();
+  apply_perm(L, w, base, g.n_p);
   // L11 (unit lower) and the 16 top rows into LDS
-  if (tid < LB * LB) {
-    const int i = tid & 15, j = tid >> 4;
-    L.L11[i][j] = A[(long long)(base + j) * g.Na + base + i];
-  }
+  if (tid < LB * LB) L.L11[tid & 15][tid >> 4] = l11;
   if (tid < LB) {
 #pragma unroll
     for (int c = 0; c < LB; ++c) L.T[tid][c] = w[0][c];
   }
   __syncthreads();
-  if (tid < LB) {                                    // column tid: forward substitution
-    for (int i = 1; i < LB; ++i) {
-      double x = L.T[i][tid];
-      for (int m2 = 0; m2 < i; ++m2) x = __builtin_fma(-L.L11[i][m2], L.T[m2][tid], x);
-      L.T[i][tid] = x;
-    }
-  }
+  trsm_lower(L);
   __syncthreads();
   if (tid < LB) {
 #pragma unroll
     for (int c = 0; c < LB; ++c) w[0][c] = L.T[tid][c];
   }
-#pragma unroll
-  for (int r = 0; r < LR; ++r) {
-    const long long row = own_row(base, r);
-    if (row < base + LB || row >= g.n_p) continue;
-#pragma unroll
-    for (int m2 = 0; m2 < LB; ++m2) {                 // one L value live at a time (<= 128 VGPRs)
-      const double l = A[(long long)(base + m2) * g.Na + row];
-#pragma unroll
-      for (int c = 0; c < LB; ++c) w[r][c] = __builtin_fma(-l, L.T[m2][c], w[r][c]);
-    }
-  }
+  r16_finish(A, g.Na, base, L, w, act, st);
   __syncthreads();                                   // L.T is rewritten by the next phase
 }
 
-// Launch k: block 0 = panel (strip k), blocks 1.. = strips k + 1 .. (update of step k-1).
-__global__ __launch_bounds__(LT) void lu_step_kernel(double* __restrict__ A, LuGeo g, int k,
-                                                     int* __restrict__ ipiv, int* __restrict__ status) {
+// Launch k: block 0 = panel (strip k), blocks 1.. = strips k + 1 .. (update of step k-1);
+// grid y = the batch slot.
+template <int LR>
+__global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k) {
   __shared__ StripLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slot = blockIdx.y;
+  double* __restrict__ A = bt.A[slot];
+  int* __restrict__ prec = bt.prec[slot];
   const int strip = k + (int)blockIdx.x;
   const int base = k > 0 ? LB * (k - 1) : 0;
   const long long c0 = (long long)LB * strip;
+  const bool stamp = blockIdx.x == 0;
+  (void)stamp;
+  if (stamp) LU_STAMP(k, 1);
+  init_maps(L);
+  __syncthreads();
   double w[LR][LB];
 #pragma unroll
   for (int r = 0; r < LR; ++r) {
     const long long row = own_row(base, r);
+    const long long rc = row < g.n_p ? row : g.n_p - 1;          // clamped: every load unconditional
 #pragma unroll
-    for (int c = 0; c < LB; ++c) w[r][c] = row < g.n_p ? A[(c0 + c) * g.Na + row] : 0.0;
+    for (int c = 0; c < LB; ++c) w[r][c] = A[(c0 + c) * g.Na + rc];
+#pragma unroll
+    for (int c = 0; c < LB; ++c) w[r][c] = row < g.n_p ? w[r][c] : 0.0;
   }
-  if (k > 0) strip_apply(A, g, ipiv, k - 1, L, w);
+  if (k > 0) strip_apply(A, g, prec + (long long)(k - 1) * PREC, k - 1, L, w);
+  if (stamp) LU_STAMP(k, 2);
   if (blockIdx.x == 0) {
-    // factor strip k: columns j, pivot rows g0 = 16 k + j (unrolled: w is indexed by j)
-#pragma unroll
+    // factor strip k: columns j, pivot rows g0 = 16 k + j.  A ROLLED loop (the unrolled one was
+    // ~60 KB of code run once per launch: instruction fetch, not arithmetic, set its 36 us), so
+    // the rows rotate instead of being indexed by j: at column j, w[r][0] is column j, w[r][c] is
+    // column j + c for c < 16 - j, and w[r][16 - j + i] is the finished column i.  Sixteen
+    // rotations restore the natural order.
+    bool singular = false;
+#pragma unroll 1
     for (int j = 0; j < LB; ++j) {
+      const int bf = j & 1;
       const long long g0 = (long long)LB * k + j;
-      double bv = -1.0;
-      long long bi = g.n_p;
+      LU_CSTAMP(k, j, 0);
+      unsigned long long bk = 0ull;
+      int brow = 0x7fffffff;
 #pragma unroll
       for (int r = 0; r < LR; ++r) {
         const long long row = own_row(base, r);
-        const double av = fabs(w[r][j]);
-        if (row >= g0 && row < g.n_p && av > bv) { bv = av; bi = row; }   // first max per thread
+        const unsigned long long kr = piv_key(w[r][0], row >= g0 && row < g.n_p);
+        if (kr > bk) { bk = kr; brow = (int)row; }                   // first max per thread
       }
+      unsigned long long wk;
+      int wrow;
+      piv_wave_best(bk, brow, wk, wrow);
+      LU_CSTAMP(k, j, 1);
 #pragma unroll
-      for (int m2 = 32; m2 > 0; m2 >>= 1) {
-        const double ov = __shfl_xor(bv, m2, 64);
-        const long long oi = __shfl_xor(bi, m2, 64);
-        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-      }
-      if (lane == 0) { L.redv[wave] = bv; L.redi[wave] = (int)bi; }
-      __syncthreads();
-      double pv = L.redv[0];
-      long long p = L.redi[0];
-      for (int u = 1; u < LT / 64; ++u)
-        if (L.redv[u] > pv || (L.redv[u] == pv && L.redi[u] < p)) { pv = L.redv[u]; p = L.redi[u]; }
-      // swap rows g0 <-> p inside the strip; prow = the pivot row
+      for (int r = 0; r < LR; ++r)
+        if (wk != 0ull && own_row(base, r) == wrow) {                  // the wave's pivot candidate row
 #pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const long long row = own_row(base, r);
-        if (row == p) {
-#pragma unroll
-          for (int c = 0; c < LB; ++c) L.prow[c] = w[r][c];
+          for (int c = 0; c < LB; ++c) L.cand[bf][wave][c] = w[r][c];
         }
+      if (lane == 0) {
+        L.ck[bf][wave] = wk;
+        L.cr[bf][wave] = wk != 0ull ? wrow : 0x7fffffff;
+      }
+#pragma unroll
+      for (int r = 0; r < LR; ++r)
+        if (own_row(base, r) == g0) {
+#pragma unroll
+          for (int c = 0; c < LB; ++c) L.grow[bf][c] = w[r][c];
+        }
+      __syncthreads();
+      LU_CSTAMP(k, j, 2);
+      unsigned long long kk[LW];
+      int rr[LW];
+#pragma unroll
+      for (int u = 0; u < LW; ++u) { kk[u] = L.ck[bf][u]; rr[u] = L.cr[bf][u]; }
+      unsigned long long pk = kk[0];
+      int p = rr[0], pw = 0;
+#pragma unroll
+      for (int u = 1; u < LW; ++u) {
+        const bool t = piv_before(kk[u], rr[u], pk, p);
+        pk = t ? kk[u] : pk;
+        p = t ? rr[u] : p;
+        pw = t ? u : pw;
+      }
+      // pk - 1 = bits of |pivot|: a zero (or NaN-only) column is singular
+      const bool zero = pk <= 1ull;
+      if (zero) { singular = true; p = (int)g0; pw = -1; }           // zero / NaN column: no swap
+      const double* prow = pw >= 0 ? L.cand[bf][pw] : L.grow[bf];
+      if (tid == 0) L.piv[j] = p;
+      const double rp = 1.0 / prow[0];
+      const int live = LB - j;                        // rotated columns 1 .. live - 1 are updated
+      double l[LR];
+      bool act[LR];
+#pragma unroll
+      for (int r = 0; r < LR; ++r) {
+        const long long row = own_row(base, r);
         if (row == g0) {
 #pragma unroll
-          for (int c = 0; c < LB; ++c) L.grow[c] = w[r][c];
-        }
-      }
-      if (tid == 0) {
-        ipiv[g0] = (int)p;
-        if (!(pv > 0.0)) atomicOr(status, 1);        // an exactly zero (or NaN) pivot: singular
-      }
-      __syncthreads();
-      const double rp = 1.0 / L.prow[j];
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const long long row = own_row(base, r);
-        if (row == g0) {
-#pragma unroll
-          for (int c = 0; c < LB; ++c) w[r][c] = L.prow[c];
+          for (int c = 0; c < LB; ++c) w[r][c] = prow[c];
         } else if (row == p) {
 #pragma unroll
-          for (int c = 0; c < LB; ++c) w[r][c] = L.grow[c];
+          for (int c = 0; c < LB; ++c) w[r][c] = L.grow[bf][c];
         }
-        if (row > g0 && row < g.n_p) {
-          const double l = w[r][j] * rp;
-          w[r][j] = l;
-#pragma unroll
-          for (int c = 0; c < LB; ++c)
-            if (c > j) w[r][c] = __builtin_fma(-l, L.prow[c], w[r][c]);
-        }
+        act[r] = row > g0 && row < g.n_p;
+        l[r] = w[r][0] * rp;
+        if (act[r]) w[r][0] = l[r];
       }
+#pragma unroll
+      for (int c = 1; c < LB; ++c)
+        if (c < live) {
+          const double pc = prow[c];                  // one LDS broadcast serves the thread's rows
+#pragma unroll
+          for (int r = 0; r < LR; ++r)
+            if (act[r]) w[r][c] = __builtin_fma(-l[r], pc, w[r][c]);
+        }
+#pragma unroll
+      for (int r = 0; r < LR; ++r) {
+        const double t = w[r][0];                     // rotate: column j goes last
+#pragma unroll
+        for (int c = 0; c + 1 < LB; ++c) w[r][c] = w[r][c + 1];
+        w[r][LB - 1] = t;
+      }
+      LU_CSTAMP(k, j, 3);
     }
+    if (tid == 0 && singular) bt.status[slot] = 1;
+    __syncthreads();                                  // L.piv complete
+    LU_STAMP(k, 3);
+    if (wave == 0) build_perm(L, k, prec + (long long)k * PREC);
+    LU_STAMP(k, 4);
   }
 #pragma unroll
   for (int r = 0; r < LR; ++r) {
@@ -261,13 +504,16 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(double* __restrict__ A, LuG
 }
 
 // ------------------------------------------------------------------------------ solve
-// out[:, 16 strip .. 16 strip + 15] = inv(A) e_col: forward with the interleaved swaps and L,
-// backward with U.  One workgroup per strip of the identity.
-__global__ __launch_bounds__(LT) void lu_solve_kernel(double* __restrict__ out, const double* __restrict__ A,
-                                                      LuGeo g, const int* __restrict__ ipiv) {
+// out[:, 16 strip .. 16 strip + 15] = inv(A) e_col: forward with the interleaved permutations
+// and L, backward with U.  One workgroup per strip of the identity (grid x) and slot (grid y).
+template <int LR>
+__global__ __launch_bounds__(LT) void lu_solve_kernel(LuBatch bt, LuGeo g) {
   __shared__ StripLds L;
   const int tid = threadIdx.x;
-  const int strip = blockIdx.x;
+  const int strip = blockIdx.x, slot = blockIdx.y;
+  const double* __restrict__ A = bt.A[slot];
+  const int* __restrict__ prec = bt.prec[slot];
+  double* __restrict__ out = bt.out[slot];
   double w[LR][LB];
 #pragma unroll
   for (int r = 0; r < LR; ++r) {
@@ -275,15 +521,42 @@ __global__ __launch_bounds__(LT) void lu_solve_kernel(double* __restrict__ out, 
 #pragma unroll
     for (int c = 0; c < LB; ++c) w[r][c] = row == (long long)LB * strip + c ? 1.0 : 0.0;
   }
-  // forward: per step the swaps, W_s = L11^-1 W_s, W_below -= L21 W_s
+  // forward: per step the permutation, W_s = L11^-1 W_s, W_below -= L21 W_s
+  init_maps(L);
+  __syncthreads();
+  int pm = 0, pp = 0, ps = 0;
+  if (tid < 32) get_perm(prec, pm, pp, ps);
+  const bool stamp = strip == 0;
+  (void)stamp;
   for (int s = 0; s < g.nbs; ++s) {
     const int b = LB * s;
-    step_perm(L, ipiv, s);
-    apply_perm(L, w, 0);
-    if (tid < LB * LB) {
-      const int i = tid & 15, j = tid >> 4;
-      L.L11[i][j] = A[(long long)(b + j) * g.Na + b + i];
+    if (stamp) LU_STAMP(s, 8);
+    // the step's loads first: L11, the first columns of L21 (the permutation record was
+    // prefetched one step ahead)
+    const double l11 = tid < LB * LB ? A[(long long)(b + (tid >> 4)) * g.Na + b + (tid & 15)] : 0.0;
+    bool act[LR];
+#pragma unroll
+    for (int r = 0; r < LR; ++r) act[r] = own_row(0, r) >= b + LB && own_row(0, r) < g.n_p;
+    R16<LR> st;
+    r16_start(A, g.Na, b, 0, act, st);
+    put_perm(L, pm, pp, ps);
+    if (tid < 32 && s + 1 < g.nbs) get_perm(prec + (long long)(s + 1) * PREC, pm, pp, ps);   // next step's, in flight
+    __syncthreads();
+    apply_perm(L, w, 0, g.n_p);
+    if (stamp) LU_STAMP(s, 9);
+    // W_s == 0 (the identity strip's rows lie below, and no pivot pulled one up): the step adds
+    // nothing -- dtrsm skips zero entries of B too (its `IF (B(K,J).NE.ZERO)`)
+    int nz = 0;
+#pragma unroll
+    for (int r = 0; r < LR; ++r) {
+      const long long row = own_row(0, r);
+      if (row >= b && row < b + LB) {
+#pragma unroll
+        for (int c = 0; c < LB; ++c) nz |= w[r][c] != 0.0;
+      }
     }
+    if (!__syncthreads_or(nz)) continue;
+    if (tid < LB * LB) L.L11[tid & 15][tid >> 4] = l11;
 #pragma unroll
     for (int r = 0; r < LR; ++r) {
       const long long row = own_row(0, r);
@@ -293,13 +566,7 @@ __global__ __launch_bounds__(LT) void lu_solve_kernel(double* __restrict__ out, 
       }
     }
     __syncthreads();
-    if (tid < LB) {
-      for (int i = 1; i < LB; ++i) {
-        double x = L.T[i][tid];
-        for (int m2 = 0; m2 < i; ++m2) x = __builtin_fma(-L.L11[i][m2], L.T[m2][tid], x);
-        L.T[i][tid] = x;
-      }
-    }
+    trsm_lower(L);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < LR; ++r) {
@@ -307,20 +574,20 @@ __global__ __launch_bounds__(LT) void lu_solve_kernel(double* __restrict__ out, 
       if (row >= b && row < b + LB) {
 #pragma unroll
         for (int c = 0; c < LB; ++c) w[r][c] = L.T[row - b][c];
-      } else if (row >= b + LB && row < g.n_p) {
-#pragma unroll
-        for (int m2 = 0; m2 < LB; ++m2) {
-          const double l = A[(long long)(b + m2) * g.Na + row];
-#pragma unroll
-          for (int c = 0; c < LB; ++c) w[r][c] = __builtin_fma(-l, L.T[m2][c], w[r][c]);
-        }
       }
     }
+    r16_finish(A, g.Na, b, L, w, act, st);
     __syncthreads();
   }
   // backward: per step from the last, W_s = U_ss^-1 W_s, W_above -= U_above,s W_s
   for (int s = g.nbs - 1; s >= 0; --s) {
     const int b = LB * s;
+    if (stamp) LU_STAMP(s, 12);
+    bool act[LR];
+#pragma unroll
+    for (int r = 0; r < LR; ++r) act[r] = own_row(0, r) < b;
+    R16<LR> st;
+    r16_start(A, g.Na, b, 0, act, st);                         // U_above,s's first columns, early
     if (tid < LB * LB) {
       const int i = tid & 15, j = tid >> 4;
       L.L11[i][j] = A[(long long)(b + j) * g.Na + b + i];     // U block (upper incl. diagonal)
@@ -334,13 +601,7 @@ __global__ __launch_bounds__(LT) void lu_solve_kernel(double* __restrict__ out, 
       }
     }
     __syncthreads();
-    if (tid < LB) {
-      for (int i = LB - 1; i >= 0; --i) {
-        double x = L.T[i][tid];
-        for (int m2 = i + 1; m2 < LB; ++m2) x = __builtin_fma(-L.L11[i][m2], L.T[m2][tid], x);
-        L.T[i][tid] = x / L.L11[i][i];
-      }
-    }
+    trsm_upper(L);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < LR; ++r) {
@@ -348,15 +609,9 @@ __global__ __launch_bounds__(LT) void lu_solve_kernel(double* __restrict__ out, 
       if (row >= b && row < b + LB) {
 #pragma unroll
         for (int c = 0; c < LB; ++c) w[r][c] = L.T[row - b][c];
-      } else if (row < b) {
-#pragma unroll
-        for (int m2 = 0; m2 < LB; ++m2) {
-          const double uu = A[(long long)(b + m2) * g.Na + row];
-#pragma unroll
-          for (int c = 0; c < LB; ++c) w[r][c] = __builtin_fma(-uu, L.T[m2][c], w[r][c]);
-        }
       }
     }
+    r16_finish(A, g.Na, b, L, w, act, st);
     __syncthreads();
   }
 #pragma unroll
@@ -382,37 +637,81 @@ LuGeo make_lu_geo(int n) {
   return g;
 }
 
+size_t slot_bytes(const LuGeo& g) {
+  return a256((size_t)g.Na * g.n_p * sizeof(double)) + a256((size_t)g.nbs * PREC * sizeof(int));
+}
+
 }  // namespace
 
-// Internal (bo_fit.hip): workspace bytes and the LU inverse of one objective (BO_OK,
-// BO_ERR_SINGULAR on an exactly zero pivot, BO_ERR_UNSUPPORTED above the register capacity).
-size_t bo_lu_workspace_size(int64_t n) {
+// Internal (bo_fit.hip): workspace bytes for `n_lu` factorisations and the LU inverses of those
+// objectives in one launch sequence (BO_OK, BO_ERR_SINGULAR on an exactly zero pivot of any of
+// them, BO_ERR_UNSUPPORTED above the register capacity).
+size_t bo_lu_workspace_size(int64_t n, int n_lu) {
   const LuGeo g = make_lu_geo((int)n);
-  return a256((size_t)g.Na * g.n_p * sizeof(double)) + a256((size_t)g.n_p * sizeof(int)) + 256;
+  return (size_t)n_lu * slot_bytes(g) + 256;
 }
 
-int bo_lu_max_n() { return LT * LR; }
+int bo_lu_max_n() { return LT * LRMAX; }
 
-int bo_lu_inverse(double* out, const double* km, int64_t ld, int64_t n, double jitter, void* ws,
-                  size_t ws_bytes, hipStream_t s) {
-  if (n < 1 || n > LT * LR) return BO_ERR_UNSUPPORTED;
-  if (ws_bytes < bo_lu_workspace_size(n)) return BO_ERR_WORKSPACE;
+int bo_lu_inverse(double* const* out, const double* const* km, int n_lu, int64_t ld, int64_t n, double jitter,
+                  void* ws, size_t ws_bytes, hipStream_t s) {
+  if (n < 1 || n > LT * LRMAX || n_lu < 1 || n_lu > BO_MAX_OBJ) return BO_ERR_UNSUPPORTED;
+  if (ws_bytes < bo_lu_workspace_size(n, n_lu)) return BO_ERR_WORKSPACE;
   const LuGeo g = make_lu_geo((int)n);
-  double* A = (double*)ws;
-  int* ipiv = (int*)((char*)ws + a256((size_t)g.Na * g.n_p * sizeof(double)));
-  int* status = (int*)((char*)ipiv + a256((size_t)g.n_p * sizeof(int)));
-  BO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
+  LuBatch bt;
+  memset(&bt, 0, sizeof(bt));
+  char* w = (char*)ws;
+  for (int b = 0; b < n_lu; ++b) {
+    bt.A[b] = (double*)w;
+    bt.prec[b] = (int*)(w + a256((size_t)g.Na * g.n_p * sizeof(double)));
+    bt.km[b] = km[b];
+    bt.out[b] = out[b];
+    w += slot_bytes(g);
+  }
+  bt.status = (int*)w;
+  BO_CHECK_HIP(hipMemsetAsync(bt.status, 0, sizeof(int) * BO_MAX_OBJ, s));
   const unsigned tiles = (unsigned)((g.n_p + 31) / 32);
-  hipLaunchKernelGGL(lu_init_kernel, dim3(tiles, tiles), dim3(256), 0, s, A, g, km, (long long)ld,
-                     jitter);
+  hipLaunchKernelGGL(lu_init_kernel, dim3(tiles, tiles, n_lu), dim3(256), 0, s, bt, g, (long long)ld, jitter);
+  // rows per thread: the fewest that hold N_p (at N = 512 one row, so no predicated-off rows)
+  const int lr = (g.n_p + LT - 1) / LT;
+  auto step = lr == 1 ? lu_step_kernel<1> : lr == 2 ? lu_step_kernel<2> : lu_step_kernel<4>;
+  auto solve = lr == 1 ? lu_solve_kernel<1> : lr == 2 ? lu_solve_kernel<2> : lu_solve_kernel<4>;
   for (int k = 0; k < g.nbs; ++k) {
     const int blocks = k > 0 ? g.nbs - k : 1;      // the panel + the strips right of it
-    hipLaunchKernelGGL(lu_step_kernel, dim3(blocks), dim3(LT), 0, s, A, g, k, ipiv, status);
+    hipLaunchKernelGGL(step, dim3(blocks, n_lu), dim3(LT), 0, s, bt, g, k);
   }
-  hipLaunchKernelGGL(lu_solve_kernel, dim3(g.nbs), dim3(LT), 0, s, out, (const double*)A, g, (const int*)ipiv);
+  hipLaunchKernelGGL(solve, dim3(g.nbs, n_lu), dim3(LT), 0, s, bt, g);
   BO_CHECK_HIP(hipGetLastError());
-  int hs = 0;
-  BO_CHECK_HIP(hipMemcpyAsync(&hs, status, sizeof(int), hipMemcpyDeviceToHost, s));
+  int hs[BO_MAX_OBJ];
+  BO_CHECK_HIP(hipMemcpyAsync(hs, bt.status, sizeof(int) * BO_MAX_OBJ, hipMemcpyDeviceToHost, s));
   BO_CHECK_HIP(hipStreamSynchronize(s));
-  return hs ? BO_ERR_SINGULAR : BO_OK;
+  for (int b = 0; b < n_lu; ++b)
+    if (hs[b]) return BO_ERR_SINGULAR;
+  return BO_OK;
 }
+
+#ifdef BO_FIT_TIMING
+// diagnostic build only: the LU stamps since the last read ([tag word, 100 MHz clock] pairs into
+// `out`, 2 cap words); resets the count and returns it
+extern "C" __attribute__((visibility("default"))) int bo_debug_lu_timing(long long* out, int cap) {
+  int cnt = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(bo_lu_tcount), sizeof(int)) != hipSuccess) return -1;
+  if (cnt > cap) cnt = cap;
+  if (cnt > 4096) cnt = 4096;
+  if (cnt > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_lu_tstamp), sizeof(long long) * 2 * cnt) != hipSuccess)
+    return -1;
+  const int zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(bo_lu_tcount), &zero, sizeof(int)) != hipSuccess) return -1;
+  return cnt;
+}
+
+// the per-column panel stamps: [step][column][4] (0 start, 1 wave max found, 2 after the
+// barrier, 3 updated and rotated)
+extern "C" __attribute__((visibility("default"))) int bo_debug_lu_cols(long long* out, int n) {
+  if (n > 64 * LB_DIAG * 4) n = 64 * LB_DIAG * 4;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_lu_cstamp), sizeof(long long) * n) != hipSuccess) return -1;
+  return n;
+}
+#endif

@@ -28,3 +28,32 @@ for _ in range(reps):
 e1.record(); torch.cuda.synchronize()
 print(f"invert_k (LU fallback) N={n} ls={ls_fit}: wall median {np.median(ts)*1e3:.3f} ms, "
       f"events {e0.elapsed_time(e1)/reps:.3f} ms per call", flush=True)
+
+# diagnostic build: the LU phase stamps of one more call (step launches: 1 start, 2 pending step
+# applied, 3 strip factored, 4 permutation record written; solve workgroup 0: 8 forward step,
+# 9 permutation applied, 12 backward step)
+lib = bo._lib.load()
+if hasattr(lib, "bo_debug_lu_timing"):
+    import ctypes
+    buf = (ctypes.c_longlong * 8192)()
+    lib.bo_debug_lu_timing(buf, 4096)
+    g(); torch.cuda.synchronize()
+    cnt = lib.bo_debug_lu_timing(buf, 4096)
+    ev = sorted((buf[2 * i + 1], buf[2 * i] >> 16, (buf[2 * i] >> 4) & 4095, buf[2 * i] & 15) for i in range(cnt))
+    t0 = ev[0][0]
+    rows = {}
+    for t, k, slot, tag in ev:
+        rows.setdefault((tag >= 8, k, slot), {})[tag] = (t - t0) * 0.01
+    for key in sorted(rows, key=lambda q: min(rows[q].values())):
+        print("solve" if key[0] else "step", key[1], "slot", key[2],
+              " ".join(f"{tag}:{v:.2f}" for tag, v in sorted(rows[key].items())))
+if hasattr(lib, "bo_debug_lu_cols"):
+    import ctypes
+    cb = (ctypes.c_longlong * 4096)()
+    lib.bo_debug_lu_cols(cb, 4096)
+    for k in (0, 1, 2):
+        print(f"panel step {k}: per column [max found, after barrier, updated] - start (us), then to next column")
+        for j in range(16):
+            b0 = (k * 16 + j) * 4
+            nxt = cb[b0 + 4] if j < 15 else cb[b0 + 3]
+            print("  col", j, " ".join(f"{(cb[b0 + t] - cb[b0]) * 0.01:.2f}" for t in (1, 2, 3)), f"{(nxt - cb[b0]) * 0.01:.2f}")

@@ -340,6 +340,35 @@ def test_invert_k_lu_path_matches_lapack(bo, n):
         assert np.abs(got[o] - ref[o]).max() <= 1e-13 * cond * scale, (o, cond)
 
 
+@pytest.mark.parametrize("n", [700, 2048])
+def test_invert_k_lu_batched_objectives(bo, n):
+    """Every objective whose Cholesky fails goes through ONE batched LU launch sequence (grid y =
+    the objective): a dense random matrix (a row swap at nearly every column), a row-permuted
+    diagonally dominant matrix (each step's 16 pivots undo a permutation: swap chains through rows
+    moved earlier in the same step), a non-symmetric kernel matrix, and one symmetric kernel
+    matrix that takes the Cholesky; each against LAPACK's inv (numba_kernels.py:401)."""
+    import torch
+    rng = np.random.default_rng(n + 1)
+    x = rng.uniform(0, 300, size=(n, 2))
+    km = np.zeros((4, n, n))
+    O.update_k(km[2:], x, 0, n, np.array([3e3, 5e2]), np.array([25.0, 40.0]))
+    km[0] = rng.standard_normal((n, n))
+    perm = rng.permutation(n)
+    km[1] = (np.diag(rng.uniform(5.0, 9.0, n)) + rng.uniform(-0.1, 0.1, size=(n, n)) / np.sqrt(n))[perm]
+    km[2] += np.triu(rng.uniform(-1e-3, 1e-3, size=(n, n)) * 3e3, 1)
+    before = bo._lib.invert_k_path_counts()
+    got = bo.kernels.invert_k(n, torch.tensor(km, device="cuda")).cpu().numpy()
+    after = bo._lib.invert_k_path_counts()
+    assert after["lu"] - before["lu"] == 3 and after["cholesky"] - before["cholesky"] == 1
+    ref = O.invert_k(n, km)
+    for o in range(4):
+        cond = np.linalg.cond(km[o] + 1e-6 * np.eye(n))
+        scale = np.abs(ref[o]).max()
+        err = np.abs(got[o] - ref[o]).max()
+        print(f"objective {o}: cond {cond:.2e}, max |d| / max |ref| {err / scale:.2e}")
+        assert err <= 1e-13 * cond * scale, (o, cond)
+
+
 def test_invert_k_lu_path_ill_conditioned(bo):
     """The regime that makes the Cholesky fail (Powell-fitted length scales drive
     cond(K + 1e-6 I) to 1e14..1e18; the reference's inv still returns): the LU path returns a
