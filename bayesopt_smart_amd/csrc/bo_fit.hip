@@ -816,7 +816,7 @@ __device__ __forceinline__ void p_tile_update(double* __restrict__ A, const Geo&
 // groups of 8 pivots plus 3 rank-8 updates, where one wave used to do all 32 columns' updates.
 __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, int o, int k, int w,
                                         double* __restrict__ part, int* __restrict__ status,
-                                        double* Cs, double* colb, double* red) {
+                                        double* Cs, double* colb, double* red, int* pflag) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const long long Na = g.Na;
@@ -920,6 +920,11 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
     }
   }
   if (stamp) FIT_STAMP(4);
+  // the panel is complete once every wave's column stores have drained: publish it now; the
+  // partials below (a log per lane, two wave reductions) only feed the host
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) st_flag(pflag, 1);
   // per-wave partials (own columns), combined through LDS
   double ldp = (lane >= c0 && lane < c0 + 8 && cK + lane < g.n) ? log(dj) : 0.0;
   double zp = 0.0;
@@ -1008,14 +1013,10 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
       __syncthreads();
       if (stamp) FIT_STAMP(2);
       if (red[15] != 0.0) {
-        p_panel(A + (long long)o * g.ostride, g, o, k, w, part, status, Cs, colb, red);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // every storing wave drains
-        __syncthreads();
-        if (tid == 0) {
-          st_flag(pf_panel(flags, g, o, k, w), 1);
-          p_panel_partials(g, o, k, w, part, status, red);
-        }
+        // publishes its completion flag itself (after its stores drain), then the partials
+        p_panel(A + (long long)o * g.ostride, g, o, k, w, part, status, Cs, colb, red, pf_panel(flags, g, o, k, w));
         if (stamp) FIT_STAMP(5);
+        if (tid == 0) p_panel_partials(g, o, k, w, part, status, red);
       }
       __syncthreads();
       continue;
