@@ -29,13 +29,17 @@ print(sys.argv[2], {k: d.get(k) for k in keys}, "frac", rf.get("frac"), "traffic
       "sel_cpu", d.get("selection_matches_cpu"), "cpu", (d.get("cpu_baseline") or {}).get("value"))
 PY
 }
-run c3_default
-run c2 --config C2
-run c4 --config C4
-run c5_fp32 --config C5
-run c5_f64 --config C5 --mode auto
-run c1 --config C1
-run iter_c3 --iteration --config C3 --steps 3 --warmup 1
-run iter_c5 --iteration --config C5 --steps 2 --warmup 1
-for c in C3 C4 C5; do run fit_$c --fit --config $c; done
-run c3_hvi --acq hvi
+[ -n "${NO_BENCH}" ] && exit 0
+if [ "${SET:-1}" = "1" ]; then
+  run c3_default
+  run c2 --config C2
+  run c4 --config C4
+  run c5_fp32 --config C5
+  run c5_f64 --config C5 --mode auto
+else
+  run c1 --config C1
+  run iter_c3 --iteration --config C3 --steps 3 --warmup 1
+  run iter_c5 --iteration --config C5 --steps 2 --warmup 1
+  for c in C3 C4 C5; do run fit_$c --fit --config $c; done
+  run c3_hvi --acq hvi
+fi
