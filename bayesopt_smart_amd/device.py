@@ -59,6 +59,11 @@ class Workspace:
         key = (device.type, device.index, int(st or 0))
         buf = cls._cache.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            # geometric growth (x1.5, 2 MiB granules): a loop whose N grows by a batch each
+            # iteration re-allocates O(log N) times, not once per iteration
+            grow = 0 if buf is None else buf.numel() + buf.numel() // 2
+            size = max(int(nbytes), grow, 256)
+            size = (size + (2 << 20) - 1) // (2 << 20) * (2 << 20) if size > (2 << 20) else size
+            buf = torch.empty(size, dtype=torch.uint8, device=device)
             cls._cache[key] = buf
         return buf
