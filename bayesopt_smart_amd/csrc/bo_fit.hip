@@ -51,6 +51,15 @@ namespace {
 constexpr int NB = 32;      // column block (panel width) and update tile
 
 // waves per SIMD the step kernel is compiled for (register budget 512 / BO_FIT_WAVES per lane)
+// launch-per-step path: write-through (sc1) stores of the panel columns and updated tiles, so
+// that no step ends with dirty L2 lines to write back at its kernel boundary
+// (r04h, N = 2048: MLL 0.966 -> 0.865 ms, inverse 1.535 -> 1.44 ms)
+#ifndef BO_FIT_WB
+constexpr int kStepStoreAux = 16;
+#else
+constexpr int kStepStoreAux = 0;
+#endif
+
 #ifndef BO_FIT_WAVES
 #define BO_FIT_WAVES 2
 #endif
@@ -93,6 +102,7 @@ struct Geo {
 __host__ __device__ inline int part_len(const Geo& g) { return 2 * g.nbt + 1; }
 
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -384,7 +394,7 @@ __device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g
       // stores kept 32 64-bit addresses live and spilled)
       // branch-free: the lanes that must not store get an offset past the resource (dropped)
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, a[j]), colr,
-                                            lane >= NB ? row_off : 0x40000000, j * col_bytes, 0);
+                                            lane >= NB ? row_off : 0x40000000, j * col_bytes, kStepStoreAux);
 #pragma unroll
       for (int t = j + 1; t < j0 + FG; ++t) a[t] = __builtin_fma(-a[j], bo_readlane_d(a[j], t), a[t]);
     }
@@ -472,6 +482,49 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
   const bool stamp_last = wt == per * g.n_obj - 1;
   if (stamp) FIT_STAMP(8);
   if (stamp_last) FIT_STAMP(10);
+#ifndef BO_FIT_U8
+  // 16-byte accesses: the MFMA rows are interleaved (A-side m -> tile column 2 m + tb, B-side n ->
+  // tile row 2 n + rb), so that each lane's two 16 x 16 blocks sit in adjacent doubles: every load
+  // and store moves a double2 (the 8-byte forms run at 0.54-0.70x the 16-byte rate)
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  dv2 cv[2][4];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      cv[tb][i] = first ? (dv2){0.0, 0.0}
+                        : *(const dv2*)(Ao + (col0 + 2 * (lg + 4 * i) + tb) * Na + row0 + 2 * li);
+  dv2 av[8], bv[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    av[ks] = *(const dv2*)(Lp + (4 * ks + lg) * Na + col0 + 2 * li);
+    bv[ks] = *(const dv2*)(Lp + (4 * ks + lg) * Na + row0 + 2 * li);
+  }
+  d4 acc[2][2];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = mfma64(av[ks][tb], bv[ks][rb], acc[tb][rb]);
+  // D[m][n] (m = lg + 4 i, n = li) of block (tb, rb) is tile element (column 2 m + tb, row 2 n + rb)
+  const int col_bytes = (int)(Na * 8);
+  const __amdgpu_buffer_rsrc_t tr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Ao + col0 * Na), (short)0, NB * col_bytes, 0x00020000);
+  const int voff = (int)(((long long)(2 * lg) * Na + row0 + 2 * li) * 8);
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const dv2 v = {cv[tb][i].x - acc[tb][0][i], cv[tb][i].y - acc[tb][1][i]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), tr, voff, (8 * i + tb) * col_bytes,
+                                             kStepStoreAux);
+    }
+#else
   // the tile's current values first (one memory round trip with the operands)
   double cv[2][2][4];
 #pragma unroll
@@ -507,27 +560,17 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        Ao[(col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li] = cv[tb][rb][i] - acc[tb][rb][i];
+      {
+        double* dst = Ao + (col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li;
+        if constexpr (kStepStoreAux != 0) __hip_atomic_store(dst, cv[tb][rb][i] - acc[tb][rb][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *dst = cv[tb][rb][i] - acc[tb][rb][i];
+      }
+#endif
 #ifdef BO_FIT_TIMING
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (stamp) FIT_STAMP(9);
   if (stamp_last) FIT_STAMP(11);
 #endif
-}
-
-// Launch k: blocks [0, n_obj * n_panel) panel role, the rest update role (4 tiles per block).
-__global__ __launch_bounds__(256, BO_FIT_WAVES) void fit_step_kernel(double* __restrict__ A, Geo g, int k, int n_panel,
-                                                       long long TL, long long TC,
-                                                       double* __restrict__ part, int* __restrict__ status) {
-  __shared__ double Cs[2 * NB * CS];
-  __shared__ double colb[NB * NB];
-  const int np = g.n_obj * n_panel;
-  if ((int)blockIdx.x < np) {
-    const int o = blockIdx.x / n_panel;
-    panel_role(A + (long long)o * g.ostride, g, o, k, blockIdx.x % n_panel, n_panel, part, status, Cs, colb);
-  } else {
-    update_role(A, g, k, TL, TC, ((long long)blockIdx.x - np) * 4 + (threadIdx.x >> 6));
-  }
 }
 
 // ---------------------------------------------------------------------------- finish
@@ -771,6 +814,47 @@ __device__ __forceinline__ void p_tile_update(double* __restrict__ A, const Geo&
   double* Ao = A + (long long)t.o * g.ostride;
   const long long Na = g.Na;
   const double* Lp = Ao + (long long)s * NB * Na;
+#ifndef BO_FIT_U8
+  // 16-byte sc1 buffer loads and stores, rows interleaved as in update_role
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  const int col_bytes = (int)(Na * 8);
+  const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc((void*)Lp, (short)0, NB * col_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t tr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Ao + col0 * Na), (short)0, NB * col_bytes, 0x00020000);
+  const int voff_t = (int)(((long long)(2 * lg) * Na + row0 + 2 * li) * 8);
+  dv2 cv[2][4];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      cv[tb][i] = t.first ? (dv2){0.0, 0.0}
+                          : __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(tr, voff_t, (8 * i + tb) * col_bytes, 16));
+  const int voff_a = (int)(((long long)lg * Na + col0 + 2 * li) * 8), voff_b = (int)(((long long)lg * Na + row0 + 2 * li) * 8);
+  dv2 av[8], bv[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    av[ks] = __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(lr, voff_a, 4 * ks * col_bytes, 16));
+    bv[ks] = __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(lr, voff_b, 4 * ks * col_bytes, 16));
+  }
+  d4 acc[2][2];
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = mfma64(av[ks][tb], bv[ks][rb], acc[tb][rb]);
+#pragma unroll
+  for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const dv2 v = {cv[tb][i].x - acc[tb][0][i], cv[tb][i].y - acc[tb][1][i]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), tr, voff_t, (8 * i + tb) * col_bytes, 16);
+    }
+#else
   double cv[2][2][4];
 #pragma unroll
   for (int tb = 0; tb < 2; ++tb)
@@ -805,6 +889,7 @@ __device__ __forceinline__ void p_tile_update(double* __restrict__ A, const Geo&
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         st_sc1(Ao + (col0 + 16 * tb + lg + 4 * i) * Na + row0 + 16 * rb + li, cv[tb][rb][i] - acc[tb][rb][i]);
+#endif
 }
 
 // The panel of step k for slab sb = k + 1 + w of objective o, on the whole workgroup: step k-1's
@@ -814,8 +899,16 @@ __device__ __forceinline__ void p_tile_update(double* __restrict__ A, const Geo&
 // (in-wave pivot chain: readlane -> rsqrt -> scale -> readlane -> fma), publishes them in LDS,
 // and every later wave applies their rank-8 update to its own columns: the critical path holds 4
 // groups of 8 pivots plus 3 rank-8 updates, where one wave used to do all 32 columns' updates.
+// SC: the persistent kernel's hand-off (sc1 loads and write-through stores, the completion flag);
+// false for the launch-per-step path, whose kernel boundaries order the steps.
+template <bool SC>
+__device__ __forceinline__ double ld_a(const double* p) {
+  if constexpr (SC) return ld_sc1(p);
+  else return *p;
+}
+
+template <bool SC>
 __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, int o, int k, int w,
-                                        double* __restrict__ part, int* __restrict__ status,
                                         double* Cs, double* colb, double* red, int* pflag) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
@@ -833,7 +926,7 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int t = 16 * tb + lg + 4 * i;
-      av_a[tb][i] = (tb < ntb && !(wave < 2 && lr0 + li < t)) ? ld_sc1(Ao + (cK + t) * Na + grow0 + li) : 0.0;
+      av_a[tb][i] = (tb < ntb && !(wave < 2 && lr0 + li < t)) ? ld_a<SC>(Ao + (cK + t) * Na + grow0 + li) : 0.0;
     }
   d4 acc[2];
   acc[0] = (d4){0.0, 0.0, 0.0, 0.0};
@@ -843,12 +936,12 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
     double av[2][8], bv[8];
     const bool zero_rows = g.ident && wave >= 2 && sb == g.nbt + k;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) bv[ks] = zero_rows ? 0.0 : ld_sc1(Lp + (4 * ks + lg) * Na + grow0 + li);
+    for (int ks = 0; ks < 8; ++ks) bv[ks] = zero_rows ? 0.0 : ld_a<SC>(Lp + (4 * ks + lg) * Na + grow0 + li);
 #pragma unroll
     for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
-        av[tb][ks] = tb < ntb ? ld_sc1(Lp + (4 * ks + lg) * Na + cK + 16 * tb + li) : 0.0;
+        av[tb][ks] = tb < ntb ? ld_a<SC>(Lp + (4 * ks + lg) * Na + cK + 16 * tb + li) : 0.0;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       acc[0] = mfma64(av[0][ks], bv[ks], acc[0]);
@@ -893,7 +986,7 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
         // and the trailing updates read only rows below it), and the other panels of this step
         // still read that tile's input values: it is not stored.
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, a[j]), colr,
-                                              lane >= NB ? row_off : 0x40000000, J * col_bytes, 16);
+                                              lane >= NB ? row_off : 0x40000000, J * col_bytes, SC ? 16 : kStepStoreAux);
 #pragma unroll
         for (int t = j + 1; t < 8; ++t) a[t] = __builtin_fma(-a[j], bo_readlane_d(a[j], 8 * p + t), a[t]);
       }
@@ -922,9 +1015,11 @@ __device__ __forceinline__ void p_panel(double* __restrict__ Ao, const Geo& g, i
   if (stamp) FIT_STAMP(4);
   // the panel is complete once every wave's column stores have drained: publish it now; the
   // partials below (a log per lane, two wave reductions) only feed the host
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) st_flag(pflag, 1);
+  if constexpr (SC) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_flag(pflag, 1);
+  }
   // per-wave partials (own columns), combined through LDS
   double ldp = (lane >= c0 && lane < c0 + 8 && cK + lane < g.n) ? log(dj) : 0.0;
   double zp = 0.0;
@@ -956,6 +1051,31 @@ __device__ __forceinline__ void p_panel_partials(const Geo& g, int o, int k, int
       if (any_bad) status[o] = 1;
     }
     if (sb == g.nbt) part[(long long)o * part_len(g) + g.nbt + k] = ((red[4] + red[5]) + red[6]) + red[7];
+  }
+}
+
+// Launch k: blocks [0, n_obj * n_panel) panel role, the rest update role (4 tiles per block).
+// SPLIT: the persistent kernel's panel (4 waves share the 32-column sweep; the MLL), else the
+// one-wave sweep (the inverse, whose nbt panels per step would crowd the trailing update's CUs:
+// r04h, N = 2048, inverse 1.60 ms split vs 1.44 one-wave; MLL 0.865 vs 0.882)
+template <bool SPLIT>
+__global__ __launch_bounds__(256, BO_FIT_WAVES) void fit_step_kernel(double* __restrict__ A, Geo g, int k, int n_panel,
+                                                       long long TL, long long TC,
+                                                       double* __restrict__ part, int* __restrict__ status) {
+  __shared__ double Cs[2 * NB * CS];
+  __shared__ double colb[SPLIT ? 3 * 64 * 8 : NB * NB];
+  __shared__ double red[16];
+  const int np = g.n_obj * n_panel;
+  if ((int)blockIdx.x < np) {
+    const int o = blockIdx.x / n_panel, w = blockIdx.x % n_panel;
+    if constexpr (SPLIT) {
+      p_panel<false>(A + (long long)o * g.ostride, g, o, k, w, Cs, colb, red, nullptr);
+      if (threadIdx.x == 0) p_panel_partials(g, o, k, w, part, status, red);
+    } else {
+      panel_role(A + (long long)o * g.ostride, g, o, k, w, n_panel, part, status, Cs, colb);
+    }
+  } else {
+    update_role(A, g, k, TL, TC, ((long long)blockIdx.x - np) * 4 + (threadIdx.x >> 6));
   }
 }
 
@@ -1014,7 +1134,7 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
       if (stamp) FIT_STAMP(2);
       if (red[15] != 0.0) {
         // publishes its completion flag itself (after its stores drain), then the partials
-        p_panel(A + (long long)o * g.ostride, g, o, k, w, part, status, Cs, colb, red, pf_panel(flags, g, o, k, w));
+        p_panel<true>(A + (long long)o * g.ostride, g, o, k, w, Cs, colb, red, pf_panel(flags, g, o, k, w));
         if (stamp) FIT_STAMP(5);
         if (tid == 0) p_panel_partials(g, o, k, w, part, status, red);
       }
@@ -1145,8 +1265,12 @@ int fit_factor(double* A, const Geo& g, const double* km, long long ld, const do
     const long long upd = ((TL + TC) * g.n_obj + 3) / 4;
     const long long grid = (long long)g.n_obj * n_panel + upd;
     if (grid == 0) continue;
-    hipLaunchKernelGGL(fit_step_kernel, dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
-                       part, status);
+    if (g.ident)
+      hipLaunchKernelGGL(fit_step_kernel<false>, dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
+                         part, status);
+    else
+      hipLaunchKernelGGL(fit_step_kernel<true>, dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
+                         part, status);
   }
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
 }
