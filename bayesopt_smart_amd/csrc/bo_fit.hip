@@ -60,6 +60,15 @@ constexpr int kStepStoreAux = 16;
 constexpr int kStepStoreAux = 0;
 #endif
 
+#if defined(BO_FIT_U8) && !defined(BO_FIT_NODEFER)
+#error "BO_FIT_U8 (8-byte tile accesses, A/B only) has no rank-64 form: build it with BO_FIT_NODEFER"
+#endif
+#ifdef BO_FIT_NODEFER
+constexpr bool kFitNoDefer = true;
+#else
+constexpr bool kFitNoDefer = false;
+#endif
+
 #ifndef BO_FIT_WAVES
 #define BO_FIT_WAVES 2
 #endif
@@ -445,7 +454,12 @@ __device__ __forceinline__ void panel_role(double* __restrict__ Ao, const Geo& g
 // [c, RB); numbered from the last column, whose count is `base`:  S(u) = u base + u (u - 1) / 2.
 __device__ __forceinline__ long long lpart_S(long long u, long long base) { return u * base + u * (u - 1) / 2; }
 
-// Update role of launch k (step s = k - 1): one 32 x 32 tile per wave.
+// Update role of launch k: one 32 x 32 tile per wave.
+//   UPD 0: step k-1 on every column block >= k+1 (and the inverse's C part)
+//   UPD 1: step k-1 on column block k+1 only (the MLL's odd launches: what the next panel needs)
+//   UPD 2: steps k-2 and k-1 together (rank 64) on every column block >= k+1 (the MLL's even
+//          launches: each trailing tile is read and written once per two steps)
+template <int UPD>
 __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g, int k, long long TL,
                                             long long TC, long long wt) {
   const int lane = threadIdx.x & 63, li = lane & 15, lg = lane >> 4;
@@ -456,7 +470,10 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
   const long long np_ = (long long)g.nbt * NB;
   long long row0, col0;
   bool first = false;
-  if (t < TL) {
+  if (UPD == 1) {
+    col0 = (long long)(k + 1) * NB;
+    row0 = (k + 1 + t) * NB;
+  } else if (t < TL) {
     const long long base = g.ident ? k + 1 : 2;
     const double bb = 2.0 * (double)base - 1.0;
     long long u = (long long)((-bb + sqrt(bb * bb + 8.0 * (double)t)) * 0.5);
@@ -477,7 +494,8 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
   }
   double* Ao = A + (long long)o * g.ostride;
   const long long Na = g.Na;
-  const double* Lp = Ao + (long long)(k - 1) * NB * Na;
+  constexpr int R = UPD == 2 ? 2 : 1;                             // steps applied
+  const double* Lp = Ao + (long long)(k - R) * NB * Na;           // L columns (k - R) * NB ..
   const bool stamp = wt == 0;
   const bool stamp_last = wt == per * g.n_obj - 1;
   if (stamp) FIT_STAMP(8);
@@ -494,9 +512,9 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
     for (int i = 0; i < 4; ++i)
       cv[tb][i] = first ? (dv2){0.0, 0.0}
                         : *(const dv2*)(Ao + (col0 + 2 * (lg + 4 * i) + tb) * Na + row0 + 2 * li);
-  dv2 av[8], bv[8];
+  dv2 av[8 * R], bv[8 * R];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
+  for (int ks = 0; ks < 8 * R; ++ks) {
     av[ks] = *(const dv2*)(Lp + (4 * ks + lg) * Na + col0 + 2 * li);
     bv[ks] = *(const dv2*)(Lp + (4 * ks + lg) * Na + row0 + 2 * li);
   }
@@ -506,7 +524,7 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) acc[tb][rb] = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks)
+  for (int ks = 0; ks < 8 * R; ++ks)
 #pragma unroll
     for (int tb = 0; tb < 2; ++tb)
 #pragma unroll
@@ -1058,7 +1076,7 @@ __device__ __forceinline__ void p_panel_partials(const Geo& g, int o, int k, int
 // SPLIT: the persistent kernel's panel (4 waves share the 32-column sweep; the MLL), else the
 // one-wave sweep (the inverse, whose nbt panels per step would crowd the trailing update's CUs:
 // r04h, N = 2048, inverse 1.60 ms split vs 1.44 one-wave; MLL 0.865 vs 0.882)
-template <bool SPLIT>
+template <bool SPLIT, int UPD>
 __global__ __launch_bounds__(256, BO_FIT_WAVES) void fit_step_kernel(double* __restrict__ A, Geo g, int k, int n_panel,
                                                        long long TL, long long TC,
                                                        double* __restrict__ part, int* __restrict__ status) {
@@ -1075,7 +1093,7 @@ __global__ __launch_bounds__(256, BO_FIT_WAVES) void fit_step_kernel(double* __r
       panel_role(A + (long long)o * g.ostride, g, o, k, w, n_panel, part, status, Cs, colb);
     }
   } else {
-    update_role(A, g, k, TL, TC, ((long long)blockIdx.x - np) * 4 + (threadIdx.x >> 6));
+    update_role<UPD>(A, g, k, TL, TC, ((long long)blockIdx.x - np) * 4 + (threadIdx.x >> 6));
   }
 }
 
@@ -1255,21 +1273,30 @@ int fit_factor(double* A, const Geo& g, const double* km, long long ld, const do
   const int steps = g.ident ? g.nbt + 1 : g.nbt;
   for (int k = 0; k < steps; ++k) {
     const int n_panel = k < g.nbt ? (g.ident ? g.nbt : g.nbt - k) : 0;
+    // the MLL defers every odd step's trailing update to the next launch (UPD 1 / 2 above)
+    const int upd_kind = g.ident || kFitNoDefer ? 0 : (k & 1) ? 1 : 2;
     long long TL = 0, TC = 0;
     if (k >= 1) {
       const long long m = g.nbt - 1 - k;
       const long long base = g.ident ? k + 1 : 2;
       TL = m > 0 ? m * base + m * (m - 1) / 2 : 0;
       TC = g.ident ? (long long)k * (k + 1) / 2 : 0;
+      if (upd_kind == 1) TL = k + 1 < g.nbt ? g.nbt - k : 0;      // tiles (k+1 .. nbt, k+1)
     }
     const long long upd = ((TL + TC) * g.n_obj + 3) / 4;
     const long long grid = (long long)g.n_obj * n_panel + upd;
     if (grid == 0) continue;
     if (g.ident)
-      hipLaunchKernelGGL(fit_step_kernel<false>, dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
+      hipLaunchKernelGGL((fit_step_kernel<false, 0>), dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
+                         part, status);
+    else if (upd_kind == 0)
+      hipLaunchKernelGGL((fit_step_kernel<true, 0>), dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
+                         part, status);
+    else if (upd_kind == 1)
+      hipLaunchKernelGGL((fit_step_kernel<true, 1>), dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
                          part, status);
     else
-      hipLaunchKernelGGL(fit_step_kernel<true>, dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
+      hipLaunchKernelGGL((fit_step_kernel<true, 2>), dim3((unsigned)grid), dim3(256), 0, s, A, g, k, n_panel, TL, TC,
                          part, status);
   }
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 TAG=${1:-r04i}
-timeout -k 10 500 python -u -m pytest tests/test_gpu_fit.py tests/test_gpu_api.py -x -q --timeout 300 --timeout-method thread -k "mll or fit or powell or cobyla or persist or invert" \
+timeout -k 10 500 python -u -m pytest tests/test_gpu_fit.py tests/test_gpu_api.py tests/test_gpu_fit_launch_path.py -x -q --timeout 300 --timeout-method thread -k "mll or fit or powell or cobyla or persist or invert or launch" \
   > gpurun_out/${TAG}_fit_tests.log 2>&1 || { echo "fit tests failed"; tail -40 gpurun_out/${TAG}_fit_tests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_fit_tests.log
 for c in ${CFGS:-C3 C4 C5}; do
