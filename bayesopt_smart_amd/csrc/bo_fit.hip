@@ -45,6 +45,7 @@
 #include <string.h>
 
 #include <vector>
+#include <chrono>
 
 namespace {
 
@@ -1099,7 +1100,8 @@ __global__ __launch_bounds__(256, BO_FIT_WAVES) void fit_step_kernel(double* __r
 
 __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict__ A, Geo g, PPlan pl,
                                                              int* __restrict__ flags, double* __restrict__ part,
-                                                             int* __restrict__ status, int* __restrict__ habort) {
+                                                             int* __restrict__ status, int* __restrict__ habort,
+                                                             int* __restrict__ hdone) {
   __shared__ double Cs[2 * NB * CS];
   __shared__ double colb[3 * 64 * 8];
   __shared__ double red[16];
@@ -1111,7 +1113,23 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
     __syncthreads();
     const int t = s_task;
     __syncthreads();                                             // s_task is rewritten next round
-    if (t >= pl.total) return;
+    if (t >= pl.total) {
+      if (hdone) {
+        // completion word in pinned host memory, stored by the last workgroup to leave after every
+        // workgroup's host-memory stores (partials, statuses, abort) drained: the host polls it
+        // instead of waiting for the kernel's completion signal
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          __threadfence_system();
+          if (atomicAdd(flags + 2, 1) == (int)gridDim.x - 1) {
+            __threadfence_system();
+            __hip_atomic_store(hdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+      }
+      return;
+    }
     // block k: blk[k] <= t < blk[k + 1]
     int lo = 0, hi = pl.steps - 1;
     while (lo < hi) {
@@ -1319,7 +1337,7 @@ int persist_max_nbt() {
 
 int fit_factor_persist(double* A, const Geo& g, const double* km, long long ld, const double* x, int dim,
                        const double* y, long long ld_y, const FitParams& p, double* part, int* status,
-                       int* flags, int* habort, hipStream_t s) {
+                       int* flags, int* habort, hipStream_t s, int* hdone = nullptr) {
   const int steps = g.ident ? g.nbt + 1 : g.nbt;
   if (steps > PMAX_STEPS || g.nbt > persist_max_nbt()) return BO_ERR_UNSUPPORTED;
   PPlan pl;
@@ -1350,7 +1368,7 @@ int fit_factor_persist(double* A, const Geo& g, const double* km, long long ld, 
                      y, ld_y, p, part, status, (int)tiles, flags, nf);
   BO_CHECK_HIP(hipGetLastError());
   const unsigned grid = (unsigned)(tot < 256 ? tot : 256);
-  hipLaunchKernelGGL(fit_persist_kernel, dim3(grid), dim3(256), 0, s, A, g, pl, flags, part, status, habort);
+  hipLaunchKernelGGL(fit_persist_kernel, dim3(grid), dim3(256), 0, s, A, g, pl, flags, part, status, habort, hdone);
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
 }
 
@@ -1365,6 +1383,25 @@ bool persist_enabled() {
   return on != 0;
 }
 long long g_fit_paths[3];     // persistent, launch-per-step, persistent aborted -> rerun
+
+// The MLL's wait for the persistent kernel: poll the completion word it stores in pinned memory
+// (BO_FIT_HOSTWAIT=sync: the stream synchronisation instead).  false when the word did not come
+// within ~0.5 s (the caller then synchronises the stream, which reports any fault).
+bool host_poll_enabled() {
+  static const int on = [] {
+    const char* e = getenv("BO_FIT_HOSTWAIT");
+    return (e && strcmp(e, "sync") == 0) ? 0 : 1;
+  }();
+  return on != 0;
+}
+bool host_poll(const int* hdone) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0;; ++i) {
+    if (__atomic_load_n(hdone, __ATOMIC_ACQUIRE) != 0) return true;
+    if ((i & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) return false;
+    __builtin_ia32_pause();
+  }
+}
 
 // how often each inverse path ran (per objective; bo_invert_k_path_counts)
 long long g_inv_paths[3];     // Cholesky, blocked LU, Gauss-Jordan
@@ -1574,12 +1611,13 @@ int bo_compute_mll_each_jitter(double* mll_obj, const double* x, int32_t dim, co
   // the per-step partials and the status flags go straight to pinned host memory (plain device
   // stores; visible after the stream synchronisation): no status memset and no read-back copy
   // per call -- two launches and their boundaries less per Powell evaluation
-  const size_t bytes = (size_t)n_obj * part_len(g) * sizeof(double) + sizeof(int) * (n_obj + 1);
+  const size_t bytes = (size_t)n_obj * part_len(g) * sizeof(double) + sizeof(int) * (n_obj + 2);
   double* h = (double*)pinned(bytes);
   if (!h) return BO_ERR_HIP;
   double* part = h;
   int* status = (int*)(part + (size_t)n_obj * part_len(g));
   int* habort = status + n_obj;
+  int* hdone = habort + 1;
   int* flags = (int*)((char*)ws + geo_bytes(g) +
                       a256((size_t)n_obj * part_len(g) * sizeof(double) + BO_MAX_OBJ * sizeof(int)) + 512);
   FitParams p;
@@ -1592,10 +1630,12 @@ int bo_compute_mll_each_jitter(double* mll_obj, const double* x, int32_t dim, co
   p.jitter = jitter;
   bool done = false;
   if (persist_enabled()) {
-    for (int o = 0; o <= n_obj; ++o) status[o] = 0;
-    const int st = fit_factor_persist(A, g, km, ld, x, dim, y, ld_y, p, part, status, flags, habort, s);
+    for (int o = 0; o <= n_obj + 1; ++o) status[o] = 0;          // statuses, abort, done
+    const bool poll = host_poll_enabled();
+    const int st = fit_factor_persist(A, g, km, ld, x, dim, y, ld_y, p, part, status, flags, habort, s,
+                                      poll ? hdone : nullptr);
     if (st == BO_OK) {
-      BO_CHECK_HIP(hipStreamSynchronize(s));
+      if (!poll || !host_poll(hdone)) BO_CHECK_HIP(hipStreamSynchronize(s));
       done = __atomic_load_n(habort, __ATOMIC_RELAXED) == 0;
       __atomic_fetch_add(&g_fit_paths[done ? 0 : 2], 1, __ATOMIC_RELAXED);
     } else if (st != BO_ERR_UNSUPPORTED) {
