@@ -48,7 +48,13 @@ def decode(t, k, nbt, ident, TL, nb):
     return np_ + b * nb, np_ + cp * nb, b == k - 1
 
 
-def step_counts(k, nbt, ident):
+def upd_kind(k, ident, defer):
+    """fit_factor's update kind of launch k: 0 = step k-1 on every live tile; for the MLL,
+    1 (odd k) = step k-1 on column block k+1 only, 2 (even k) = steps k-2 and k-1 (rank 64)."""
+    return 0 if (ident or not defer) else (1 if k & 1 else 2)
+
+
+def step_counts(k, nbt, ident, defer=False):
     """fit_factor's per-launch counts: panel workgroups, L-part and C-part update tiles."""
     n_panel = (nbt if ident else nbt - k) if k < nbt else 0
     TL = TC = 0
@@ -57,17 +63,21 @@ def step_counts(k, nbt, ident):
         base = k + 1 if ident else 2
         TL = m * base + m * (m - 1) // 2 if m > 0 else 0
         TC = k * (k + 1) // 2 if ident else 0
+        if upd_kind(k, ident, defer) == 1:
+            TL = nbt - k if k + 1 < nbt else 0
     return n_panel, TL, TC
 
 
-def fit_schedule(A, n, nb, ident):
-    """bo_fit.hip fit_factor on one objective (tile nb), in place; returns False on a bad pivot."""
+def fit_schedule(A, n, nb, ident, defer=False):
+    """bo_fit.hip fit_factor on one objective (tile nb), in place; returns False on a bad pivot.
+    defer: the MLL's schedule (update_role<1> on odd launches, update_role<2> on even ones)."""
     nbt = -(-n // nb)
     np_ = nbt * nb
     ok = True
     steps = nbt + 1 if ident else nbt
     for k in range(steps):
-        n_panel, TL, TC = step_counts(k, nbt, ident)
+        n_panel, TL, TC = step_counts(k, nbt, ident, defer)
+        kind = upd_kind(k, ident, defer)
         old = A.copy()                          # every role of launch k reads the launch's input
         cK, cP = k * nb, (k - 1) * nb
         for w in range(n_panel):                # panel role: diagonal tile + slab block sb
@@ -89,15 +99,22 @@ def fit_schedule(A, n, nb, ident):
                 A[cK:cK + nb, cK:cK + nb] = np.tril(L) + np.triu(old[cK:cK + nb, cK:cK + nb], 1)
             A[sb * nb:sb * nb + nb, cK:cK + nb] = np.linalg.solve(L, C[nb:].T).T
         tiles = set()
-        for t in range(TL + TC):                # update role: step k-1 on every live tile
-            r0, c0, first = decode(t, k, nbt, ident, TL, nb)
+        R = 2 if kind == 2 else 1               # steps applied by this launch's update role
+        cS = (k - R) * nb
+        for t in range(TL + TC):                # update role
+            if kind == 1:
+                r0, c0, first = (k + 1 + t) * nb, (k + 1) * nb, False
+            else:
+                r0, c0, first = decode(t, k, nbt, ident, TL, nb)
             assert (r0, c0) not in tiles
             tiles.add((r0, c0))
-            upd = old[r0:r0 + nb, cP:cP + nb] @ old[c0:c0 + nb, cP:cP + nb].T
+            upd = old[r0:r0 + nb, cS:cS + R * nb] @ old[c0:c0 + nb, cS:cS + R * nb].T
             A[r0:r0 + nb, c0:c0 + nb] = (0.0 if first else old[r0:r0 + nb, c0:c0 + nb]) - upd
+        if kind == 1 and k >= 1:
+            assert tiles == {(r * nb, (k + 1) * nb) for r in range(k + 1, nbt + 1)} if k + 1 < nbt else not tiles
         # the live set the decode enumerates: L part (columns > k, rows from the diagonal to the
         # live bottom) and, for the inverse, C's lower tiles of the live bottom blocks
-        if k >= 1:
+        elif k >= 1:
             rb_hi = nbt + (k if ident else 1)
             want = {(r * nb, c * nb) for c in range(k + 1, nbt) for r in range(c, rb_hi)}
             if ident:
@@ -140,8 +157,9 @@ def test_augmented_inverse_schedule(n, nb):
     assert np.abs(got - ref).max() <= 1e-9 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("n,nb", [(5, 4), (37, 8), (100, 32), (70, 8)])
-def test_augmented_mll_schedule(n, nb):
+@pytest.mark.parametrize("defer", [False, True])
+@pytest.mark.parametrize("n,nb", [(5, 4), (37, 8), (100, 32), (70, 8), (60, 4), (64, 4)])
+def test_augmented_mll_schedule(n, nb, defer):
     rng = np.random.default_rng(n + 1)
     x = rng.uniform(0, 30, size=(n, 2))
     y = rng.normal(size=(n, 2)) * 10
@@ -154,7 +172,7 @@ def test_augmented_mll_schedule(n, nb):
     for o in range(2):
         yc = y[:, o] - pm[o]                    # unscaled: |z|^2 / var(yc) is the data fit
         A, np_ = build(km[o] / pv[o], n, nb, False, 1e-8, yc)
-        assert fit_schedule(A, n, nb, False)
+        assert fit_schedule(A, n, nb, False, defer)
         z = A[np_, :np_]
         fit = float(np.sum(z * z)) / np.var(yc)
         logdet = 2.0 * np.sum(np.log(np.diag(A)[:n]))
