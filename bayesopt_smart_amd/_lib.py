@@ -22,7 +22,7 @@ MAX_TOPQ = 48
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_WORKSPACE, ERR_HIP, ERR_NOT_PD, ERR_SINGULAR = range(7)
 CAND_I64, CAND_F64, CAND_GRID, CAND_SOBOL = 0, 1, 2, 3
-ABI_VERSION = 3
+ABI_VERSION = 4
 MODE_AUTO, MODE_DENSE, MODE_NO_SEPARABLE, MODE_FP32, MODE_F32_FLOOR = 0, 1, 2, 4, 8
 
 c_dbl_p = C.POINTER(C.c_double)
@@ -119,6 +119,8 @@ _SIGS = {
     "bo_invert_k_workspace_size": (C.c_size_t, [C.c_int32, C.c_int64]),
     "bo_invert_k_jitter": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, C.c_double, c_vp,
                                      C.c_size_t, c_vp]),
+    "bo_invert_k_ex": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int32, C.c_int64, C.c_double,
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32), c_vp, C.c_size_t, c_vp]),
     "bo_compute_mll_each_jitter": (C.c_int, [c_dbl_p, c_vp, C.c_int32, c_vp, C.c_int64, c_vp, C.c_int64,
                                              C.c_int32, c_dbl_p, c_dbl_p, c_dbl_p, C.c_int64, C.c_double,
                                              c_vp, C.c_size_t, c_vp]),

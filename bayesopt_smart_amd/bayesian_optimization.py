@@ -88,8 +88,8 @@ def _broadcast_np(arr, group=None, device=None):
     collective's tensor lives where the backend needs it: on `device` (the backend's HIP device,
     default the current one) for RCCL, on the host for gloo."""
     import torch.distributed as dist
-    _, world = _world(group)
-    if world == 1 or np.size(arr) == 0:
+    from .distributed import collectives_on
+    if not collectives_on(group) or np.size(arr) == 0:
         return arr
     if dist.get_backend(group) == "nccl":
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -131,6 +131,8 @@ class DeviceBackend:
         if buffers is None:
             buffers = DeviceBuffers(n_obj, total_samples, self.count, self.dev)
         self.bufs = buffers
+        self._lu_hint = None           # per objective: the previous invert_k took the LU path
+        self.inverse_paths = []
 
     def fit(self, x_vector, y_vector, n, prior_mean, prior_variance, length_scales):
         """Returns (Powell's OptimizeResult, fitted device state, time after the Powell fit)."""
@@ -142,7 +144,14 @@ class DeviceBackend:
         _broadcast_np(prior_variance, self.group, self.dev)
         t1 = time.perf_counter()
         K.update_k(self.bufs.kernel_matrices, xd, 0, n, prior_variance, length_scales)
-        kinv = K.invert_k(n, self.bufs.kernel_matrices, float_type=self.float_type)
+        # an objective whose Cholesky failed last iteration (Powell-fitted length scales drive
+        # cond(K + 1e-6 I) past 1e16) fails again: when all did, go straight to the
+        # blocked LU -- gesv's algorithm, the reference's own -- without the doomed attempt
+        paths = []
+        kinv = K.invert_k(n, self.bufs.kernel_matrices, float_type=self.float_type, lu_hint=self._lu_hint,
+                          paths=paths)
+        self._lu_hint = [p != 0 for p in paths]
+        self.inverse_paths = paths
         torch.cuda.synchronize(self.dev)
         return optimized, (xd, yd, kinv), t1
 
@@ -178,10 +187,10 @@ class DeviceBackend:
                                      len(y_evaluated), reference_point, prior_mean, prior_variance,
                                      self.cands, evaluated, batch_size, offset=self.offset,
                                      return_record=True)
-            if self.world == 1:
+            from .distributed import collectives_on, exchange_topq_rec
+            if not collectives_on(self.group):
                 idx = rec[batch_size:].view(torch.int64).cpu().numpy()
                 return idx[idx >= 0]
-            from .distributed import exchange_topq_rec
             return np.asarray(exchange_topq_rec(rec, batch_size, self.group)[1], dtype=np.int64)
         if acquisition == "hvi":
             update_hypervolume_improvement_exact(self.bufs.acquisition_values, self.bufs.ucb, y_evaluated,
@@ -189,7 +198,8 @@ class DeviceBackend:
                                                  prior_variance)
         # batches above BO_MAX_TOPQ: rounds of the standalone device selection (over the gathered
         # array when sharded)
-        acq = self.bufs.acquisition_values if self.world == 1 else \
+        from .distributed import collectives_on
+        acq = self.bufs.acquisition_values if not collectives_on(self.group) else \
             torch.as_tensor(self.state_arrays()["acquisition_values"], device=self.dev)
         return select_indices(acq, self.cands, evaluated, batch_size)
 
@@ -197,9 +207,9 @@ class DeviceBackend:
         b = self.bufs
         arrs = {"mu_objectives": b.mu_objectives, "variance_objectives": b.variance_objectives,
                 "acquisition_values": b.acquisition_values}
-        if self.world == 1:
+        from .distributed import collectives_on, gather_shards
+        if not collectives_on(self.group):
             return arrs
-        from .distributed import gather_shards
         return {k: gather_shards(v, self.cands.n, self.group) for k, v in arrs.items()}
 
 
@@ -255,11 +265,18 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
         backend = DeviceBackend(cands, n_obj, total_samples, dev, bufs, group, float_type=float_type)
     cands, rank, world = backend.cands, backend.rank, backend.world
     gather = bool(callbacks)
-    if world > 1:                       # any rank with callbacks: every rank joins the gathers
+    bgroup = getattr(backend, "group", group)
+    from .distributed import collectives_on
+    coll = collectives_on(bgroup)
+    if coll:                            # any rank with callbacks: every rank joins the gathers
         import torch.distributed as dist
-        flag = torch.tensor([1.0 if callbacks else 0.0], dtype=torch.float64,
-                            device=backend.dev if dist.get_backend(backend.group) == "nccl" else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=backend.group)
+        if dist.get_backend(bgroup) == "nccl":      # RCCL: the flag on the backend's HIP device
+            bdev = getattr(backend, "dev", None)
+            fdev = torch.device(bdev) if bdev is not None else torch.device("cuda", torch.cuda.current_device())
+        else:
+            fdev = torch.device("cpu")
+        flag = torch.tensor([1.0 if callbacks else 0.0], dtype=torch.float64, device=fdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=bgroup)
         gather = bool(flag.item())
 
     last_eval = 0
@@ -277,8 +294,8 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
             x_vector[current_eval + b_idx] = point
             if rank == 0:       # the user's objective, once per point (bayesian_optimization.py:213-216)
                 y_vector[current_eval + b_idx] = function(point)
-        if world > 1:
-            _broadcast_np(y_vector[current_eval:current_eval + len(x_next)], backend.group,
+        if coll:
+            _broadcast_np(y_vector[current_eval:current_eval + len(x_next)], bgroup,
                           getattr(backend, "dev", None))
         last_eval = current_eval
         t4 = time.perf_counter()

@@ -596,7 +596,8 @@ __device__ __forceinline__ void update_role(double* __restrict__ A, const Geo& g
 // out[o][i][j] = -C[max(i, j)][min(i, j)] (C = the bottom-right block, lower triangle): the
 // symmetric K^-1.  32 x 32 output tiles: lower tiles read C column-major (coalesced), upper tiles
 // the mirrored lower tile through LDS; writes are row-major.
-__global__ __launch_bounds__(256) void inv_extract_kernel(double* __restrict__ out, const double* __restrict__ A,
+__global__ __launch_bounds__(256) void inv_extract_kernel(double* __restrict__ out, long long out_stride,
+                                                          const double* __restrict__ A,
                                                           Geo g, const int* __restrict__ status) {
   __shared__ double tile[NB][NB + 1];
   const int o = blockIdx.z;
@@ -604,6 +605,7 @@ __global__ __launch_bounds__(256) void inv_extract_kernel(double* __restrict__ o
   const int bi = blockIdx.y, bj = blockIdx.x;   // output tile (rows 32 bi, columns 32 bj)
   const long long np_ = (long long)g.nbt * NB;
   const double* Ao = A + (long long)o * g.ostride;
+  out += (long long)o * out_stride;
   const long long n = g.n;
   const int lo = bi >= bj ? bi : bj, hi = bi >= bj ? bj : bi;   // source lower tile (lo, hi)
   const int tid = threadIdx.x, c = tid >> 5, r = tid & 31;
@@ -622,8 +624,105 @@ __global__ __launch_bounds__(256) void inv_extract_kernel(double* __restrict__ o
     // element (i, j): lower (i >= j) -> C(i, j) = tile[j - 32 hi][i - 32 lo] with lo = bi
     const long long gr = i >= j ? i : j, gc = i >= j ? j : i;
     const double v = tile[gc - (long long)hi * NB][gr - (long long)lo * NB];
-    out[(long long)o * n * n + i * n + j] = -v;
+    out[i * n + j] = -v;
   }
+}
+
+// 64 wait states between the last MFMA writing the accumulators and their first VALU read (the
+// round-1 gfx950 hazard)
+__device__ __forceinline__ void mfma_fence_acc(d4 (&acc)[2][2]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+               : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]));
+}
+
+// --------------------------------------------------------------- inverse refinement
+// One Newton step on the Cholesky-path inverse, X' = X + X (I - A X) with A = K + jitter I: the
+// residual I - A X' is (I - A X)^2 up to the rounding of the two products, so X' carries the
+// residual of a backward-stable solve (LAPACK gesv's, the reference's np.linalg.inv,
+// numba_kernels.py:401) where the product form L^-T L^-1 of the factorisation alone was 12x (N =
+// 512) to 144x (N = 2048) above it (round-4 GPU log).  Two MFMA GEMMs per objective:
+//   MODE 0:  R = I - (K + jitter I) X          (A operand: the caller's K, leading dimension ld)
+//   MODE 1:  out = X + X R                     (A operand: X)
+// Both A operands are symmetric (the Cholesky path runs only for a symmetric K; X is the
+// mirrored lower triangle), so A[i][k] is read as A[k][i]: every operand load is 16 consecutive
+// doubles of a row.  64 x 64 output tile per workgroup, 32 x 32 per wave (2 x 2
+// v_mfma_f64_16x16x4_f64 blocks), k in blocks of 32 with the next block's loads in flight.
+template <int MODE>
+__global__ __launch_bounds__(256) void inv_refine_kernel(const double* __restrict__ Am, long long lda, long long a_os,
+                                                         double jitter, const double* __restrict__ Bm,
+                                                         long long b_os, const double* __restrict__ Xm,
+                                                         long long x_os, double* __restrict__ D, long long d_os,
+                                                         int n, const int* __restrict__ status) {
+  const int o = blockIdx.z;
+  if (status[o]) return;                        // LU objective: refined by nothing (gesv itself)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int i0 = blockIdx.y * 64 + (wave >> 1) * 32, j0 = blockIdx.x * 64 + (wave & 1) * 32;
+  if (i0 >= n || j0 >= n) return;               // wave-uniform; no barriers below
+  const double* Ao = Am + (long long)o * a_os;
+  const double* Bo = Bm + (long long)o * b_os;
+  const long long ldb = n;
+  bool ca[2], cb[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    ca[t] = i0 + 16 * t + li < n;
+    cb[t] = j0 + 16 * t + li < n;
+  }
+  constexpr int KS = 8;                         // k-steps (of 4) per block
+  double av[2][KS][2], bv[2][KS][2];
+  auto load = [&](int buf, int kb) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = kb + 4 * s + lg;
+      const bool kok = k < n;
+      const double* ra = Ao + (long long)k * lda;
+      const double* rb = Bo + (long long)k * ldb;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ci = i0 + 16 * t + li, cj = j0 + 16 * t + li;
+        double a = (kok && ca[t]) ? ra[ci] : 0.0;
+        if (MODE == 0 && k == ci) a += jitter;   // numba_kernels.py:397-398
+        av[buf][s][t] = a;
+        bv[buf][s][t] = (kok && cb[t]) ? rb[cj] : 0.0;
+      }
+    }
+  };
+  d4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma64(av[buf][s][a], bv[buf][s][b], acc[a][b]);
+  };
+  // ping-pong with static buffer indices (a variable index puts the arrays in scratch)
+  load(0, 0);
+  for (int kb = 0; kb < n; kb += 8 * KS) {
+    if (kb + 4 * KS < n) load(1, kb + 4 * KS);
+    compute(0);
+    if (kb + 4 * KS >= n) break;
+    if (kb + 8 * KS < n) load(0, kb + 8 * KS);
+    compute(1);
+  }
+  mfma_fence_acc(acc);
+  const double* Xo = Xm + (long long)o * x_os;
+  double* Do = D + (long long)o * d_os;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 16 * a + lg + 4 * r, j = j0 + 16 * b + li;
+        if (i >= n || j >= n) continue;
+        const long long e = (long long)i * n + j;
+        Do[e] = MODE == 0 ? ((i == j ? 1.0 : 0.0) - acc[a][b][r]) : Xo[e] + acc[a][b][r];
+      }
 }
 
 // ------------------------------------------------------------- LU fallback (invert_k)
@@ -743,6 +842,7 @@ constexpr int PMAX_STEPS = 128;
 
 struct PPlan {
   int steps, total;
+  int force_abort;                           // test-only (BO_FIT_TEST_ABORT=1): abort at once
   int blk[PMAX_STEPS + 1];                   // first task of block k
 };
 
@@ -1108,6 +1208,11 @@ __global__ __launch_bounds__(256, 2) void fit_persist_kernel(double* __restrict_
   __shared__ int s_task;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int* abort_w = flags + 1;
+  if (pl.force_abort && blockIdx.x == 0 && tid == 0) {
+    // the recovery path under test: every wait that has to spin gives up, the host reruns
+    st_flag(abort_w, 1);
+    *habort = 1;
+  }
   while (true) {
     if (tid == 0) s_task = atomicAdd(flags, 1);                  // dequeue (returning atomic)
     __syncthreads();
@@ -1320,6 +1425,16 @@ int fit_factor(double* A, const Geo& g, const double* km, long long ld, const do
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
 }
 
+// BO_FIT_TEST_ABORT=1 (tests only): every persistent launch raises its abort word at once, so
+// that the host's rerun on the launch-per-step path runs (tests/test_gpu_fit_abort.py)
+bool test_abort_enabled() {
+  static const int on = [] {
+    const char* e = getenv("BO_FIT_TEST_ABORT");
+    return (e && strcmp(e, "1") == 0) ? 1 : 0;
+  }();
+  return on != 0;
+}
+
 // The persistent path: init launch (which also zeroes the flag words) + ONE fit_persist_kernel
 // launch.  BO_ERR_UNSUPPORTED when the task list exceeds PMAX_STEPS blocks (the caller uses
 // fit_factor).  *habort (host-visible) is set when a wait gave up: the caller reruns fit_factor.
@@ -1343,6 +1458,7 @@ int fit_factor_persist(double* A, const Geo& g, const double* km, long long ld, 
   PPlan pl;
   memset(&pl, 0, sizeof(pl));
   pl.steps = steps;
+  pl.force_abort = test_abort_enabled() ? 1 : 0;
   long long tot = 0;
   for (int k = 0; k < steps; ++k) {
     pl.blk[k] = (int)tot;
@@ -1406,6 +1522,38 @@ bool host_poll(const int* hdone) {
 // how often each inverse path ran (per objective; bo_invert_k_path_counts)
 long long g_inv_paths[3];     // Cholesky, blocked LU, Gauss-Jordan
 
+// BO_INV_REFINE=0 leaves the Cholesky-path inverse unrefined (A/B measurements only)
+bool refine_enabled() {
+  static const int on = [] {
+    const char* e = getenv("BO_INV_REFINE");
+    return (e && strcmp(e, "0") == 0) ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// The Cholesky path's result: -C mirrored into X (the dead first columns of each objective's
+// augmented matrix), then one Newton step X + X (I - (K + jitter I) X) into `out`
+// (inv_refine_kernel).  Objectives whose factorisation failed are skipped on the device.
+int inv_finish(double* out, double* A, const Geo& g, const double* km, long long ld, double jitter,
+               const int* status, hipStream_t s) {
+  const unsigned nt = (unsigned)g.nbt;
+  const long long n = g.n;
+  if (!refine_enabled()) {
+    hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, g.n_obj), dim3(256), 0, s, out, n * n, A, g, status);
+    return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
+  }
+  double* X = A;                               // objective o: X at A_o, R at A_o + n^2 (< 2 n_p^2)
+  double* R = A + n * n;
+  hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, g.n_obj), dim3(256), 0, s, X, g.ostride, A, g, status);
+  const unsigned t64 = (unsigned)((n + 63) / 64);
+  hipLaunchKernelGGL(inv_refine_kernel<0>, dim3(t64, t64, g.n_obj), dim3(256), 0, s, km, ld, ld * ld, jitter,
+                     (const double*)X, g.ostride, (const double*)nullptr, 0ll, R, g.ostride, (int)n, status);
+  hipLaunchKernelGGL(inv_refine_kernel<1>, dim3(t64, t64, g.n_obj), dim3(256), 0, s, (const double*)X, n,
+                     g.ostride, 0.0, (const double*)R, g.ostride, (const double*)X, g.ostride, out, n * n, (int)n,
+                     status);
+  return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
+}
+
 // pinned staging for the per-call read-back (one per host thread)
 void* pinned(size_t bytes) {
   thread_local void* buf = nullptr;
@@ -1439,6 +1587,11 @@ int bo_invert_k(double* out, const double* km, int64_t ld, int32_t n_obj, int64_
 
 int bo_invert_k_jitter(double* out, const double* km, int64_t ld, int32_t n_obj, int64_t n, double jitter,
                        void* ws, size_t ws_bytes, void* stream) {
+  return bo_invert_k_ex(out, km, ld, n_obj, n, jitter, nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+int bo_invert_k_ex(double* out, const double* km, int64_t ld, int32_t n_obj, int64_t n, double jitter,
+                   const int32_t* lu_hint, int32_t* path_out, void* ws, size_t ws_bytes, void* stream) {
   if (!out || !km || n_obj < 1 || n_obj > BO_MAX_OBJ || n < 1 || ld < n) return BO_ERR_ARG;
   if (n > (1 << 15)) return BO_ERR_UNSUPPORTED;
   if (!ws || ws_bytes < bo_invert_k_workspace_size(n_obj, n)) return BO_ERR_WORKSPACE;
@@ -1458,6 +1611,16 @@ int bo_invert_k_jitter(double* out, const double* km, int64_t ld, int32_t n_obj,
   FitParams p;
   memset(&p, 0, sizeof(p));
   p.jitter = jitter;
+  int fail[BO_MAX_OBJ], path[BO_MAX_OBJ];
+  bool all_lu = lu_hint != nullptr;
+  for (int o = 0; o < n_obj; ++o) {
+    path[o] = 0;
+    if (all_lu && lu_hint[o] == 0) all_lu = false;
+  }
+  if (all_lu) {
+    // every objective's Cholesky failed last time (the caller's hint): no doomed attempt
+    for (int o = 0; o < n_obj; ++o) fail[o] = 1;
+  } else {
   int* hstat = (int*)pinned(sizeof(int) * (BO_MAX_OBJ + 4));
   if (!hstat) return BO_ERR_HIP;
   bool done = false;
@@ -1465,9 +1628,9 @@ int bo_invert_k_jitter(double* out, const double* km, int64_t ld, int32_t n_obj,
     BO_CHECK_HIP(hipMemsetAsync(status, 0, 256, s));
     const int st = fit_factor_persist(A, g, km, ld, nullptr, 0, nullptr, 0, p, nullptr, status, flags, dabort, s);
     if (st == BO_OK) {
-      const unsigned nt = (unsigned)g.nbt;
-      hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, n_obj), dim3(256), 0, s, out, A, g, status);
-      BO_CHECK_HIP(hipGetLastError());
+      // after an abort the statuses are incomplete: the rerun below redoes the whole call
+      const int st_f = inv_finish(out, A, g, km, ld, jitter, status, s);
+      if (st_f != BO_OK) return st_f;
       BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * (BO_MAX_OBJ + 4), hipMemcpyDeviceToHost, s));
       BO_CHECK_HIP(hipStreamSynchronize(s));
       done = hstat[BO_MAX_OBJ + 2] == 0;
@@ -1481,17 +1644,17 @@ int bo_invert_k_jitter(double* out, const double* km, int64_t ld, int32_t n_obj,
     BO_CHECK_HIP(hipMemsetAsync(status, 0, 256, s));
     int st = fit_factor(A, g, km, ld, nullptr, 0, nullptr, 0, p, nullptr, status, s);
     if (st != BO_OK) return st;
-    const unsigned nt = (unsigned)g.nbt;
-    hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, n_obj), dim3(256), 0, s, out, A, g, status);
-    BO_CHECK_HIP(hipGetLastError());
+    const int st_f = inv_finish(out, A, g, km, ld, jitter, status, s);
+    if (st_f != BO_OK) return st_f;
     BO_CHECK_HIP(hipMemcpyAsync(hstat, status, sizeof(int) * n_obj, hipMemcpyDeviceToHost, s));
     BO_CHECK_HIP(hipStreamSynchronize(s));
   }
-  int fail[BO_MAX_OBJ];
   for (int o = 0; o < n_obj; ++o) {
     fail[o] = hstat[o];
     if (!fail[o]) __atomic_fetch_add(&g_inv_paths[0], 1, __ATOMIC_RELAXED);
   }
+  }   // Cholesky attempt
+  for (int o = 0; o < n_obj; ++o) path[o] = fail[o] ? 1 : 0;
   // LU path for the objectives whose Cholesky failed or whose K is not symmetric: the blocked
   // LU with partial pivoting of bo_lu.hip, all of them in one launch sequence, in the (now free)
   // augmented-matrix region; Gauss-Jordan with partial pivoting above its register capacity
@@ -1509,6 +1672,9 @@ int bo_invert_k_jitter(double* out, const double* km, int64_t ld, int32_t n_obj,
       for (int o = 0; o < n_obj; ++o) fail[o] = 0;
     }
   }
+  for (int o = 0; o < n_obj; ++o) path[o] = fail[o] ? 2 : path[o];
+  if (path_out)
+    for (int o = 0; o < n_obj; ++o) path_out[o] = path[o];
   for (int o = 0; o < n_obj; ++o) {
     if (!fail[o]) continue;
     __atomic_fetch_add(&g_inv_paths[2], 1, __ATOMIC_RELAXED);

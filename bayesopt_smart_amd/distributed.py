@@ -9,11 +9,23 @@ reference's selection order.  Payload P * q * 16 bytes -- latency-bound over xGM
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from .predict import merge_topq, predict_acquire
+
+
+def collectives_on(group=None):
+    """True when the exchange steps run as collectives: torch.distributed is initialised and the
+    group has several ranks -- or BO_FORCE_COLLECTIVES=1, which runs every collective of the loop
+    and the bench on a single rank too (tests/test_gpu_rccl_one_rank.py executes the RCCL path on
+    one GPU that way)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(group) > 1 or os.environ.get("BO_FORCE_COLLECTIVES") == "1"
 
 
 def shard_range(n, rank, world):
@@ -86,7 +98,7 @@ def front_hypervolume(front, reference_point, group=None, device=None, partial=N
         ub = (ctypes.c_double * r.size)(*upper.tolist())
         _lib.check(_lib.load().bo_box_volume_sum(bd.data_ptr() if bd.numel() else None, mine.shape[0], r.size,
                                                  ub, val.data_ptr(), stream_handle(dev)), "bo_box_volume_sum")
-    if world > 1:
+    if collectives_on(group):
         if dist.get_backend(group) != "nccl":
             val = val.cpu()
         dist.all_reduce(val, op=dist.ReduceOp.SUM, group=group)
@@ -140,7 +152,7 @@ def sharded_predict_acquire(x_train, y_train, kinv, cands, prior_mean, prior_var
         kw["float_type"] = float_type
     r = score(x_train, y_train, kinv, cands, prior_mean, prior_variance, length_scales, betas,
               outputs=outputs, topq=q, offset=off, count=cnt, **kw)
-    if world == 1:
+    if not collectives_on(group):
         sel = merge_topq(r["top_val"].cpu().numpy(), r["top_idx"].cpu().numpy(), q)
     else:
         sel = exchange_topq_rec(kw["top_rec"], q, group)

@@ -121,12 +121,17 @@ def update_k(kernel_matrix, x_vector, last_eval, current_eval, prior_variance, l
     km.finish()
 
 
-def invert_k(current_eval, kernel_matrix, *, float_type=None):
+def invert_k(current_eval, kernel_matrix, *, float_type=None, lu_hint=None, paths=None):
     """numba_kernels.py:370-403 — inv(K[:N,:N] + KERNEL_JITTER I) per objective (1e-6; 1e-3 in the
-    float32 branch): Cholesky, or the blocked LU with partial pivoting when it fails.
+    float32 branch): Cholesky plus one Newton step, or the blocked LU with partial pivoting when it
+    fails.
 
     Returns a new array of the caller's kind (numpy in, numpy out; tensor in, tensor out).
     Raises numpy.linalg.LinAlgError on an exactly singular pivot.
+    `lu_hint` (per-objective booleans, optional): when all are true the Cholesky attempt is
+    skipped and every objective takes the LU path (a loop whose previous iteration's Cholesky
+    failed for them).  `paths` (a list, optional) receives the per-objective path taken:
+    0 Cholesky, 1 blocked LU, 2 Gauss-Jordan.
     """
     dev = _dev_of(kernel_matrix)
     km = _Arg(kernel_matrix, dev)
@@ -136,8 +141,14 @@ def invert_k(current_eval, kernel_matrix, *, float_type=None):
     lib = _lib.load()
     ws = Workspace.get(lib.bo_invert_k_workspace_size(n_obj, n), dev)
     jitter = precision_constants(float_type)[0]
-    _lib.check(lib.bo_invert_k_jitter(out.data_ptr(), km.ptr, ld, n_obj, n, jitter, ws.data_ptr(), ws.numel(),
-                                      stream_handle(dev)), "bo_invert_k")
+    hint = None
+    if lu_hint is not None:
+        hint = (C.c_int32 * n_obj)(*[1 if lu_hint[o] else 0 for o in range(n_obj)])
+    taken = (C.c_int32 * n_obj)()
+    _lib.check(lib.bo_invert_k_ex(out.data_ptr(), km.ptr, ld, n_obj, n, jitter, hint, taken, ws.data_ptr(),
+                                  ws.numel(), stream_handle(dev)), "bo_invert_k")
+    if paths is not None:
+        paths[:] = [int(taken[o]) for o in range(n_obj)]
     return out if isinstance(kernel_matrix, torch.Tensor) else out.cpu().numpy()
 
 

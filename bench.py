@@ -583,6 +583,9 @@ def main():
     # BO_BENCH_BACKEND=gloo: a functional rehearsal of the multi-rank step with several ranks on
     # one device (not a measurement); the product launch is one rank per GPU over RCCL
     backend = os.environ.get("BO_BENCH_BACKEND", "nccl")
+    # BO_FORCE_COLLECTIVES=1 with WORLD_SIZE=1 (torch.distributed.run --nproc-per-node 1): the
+    # process group and every exchange of the step run on one rank (tests/test_gpu_rccl_one_rank.py)
+    use_dist = world > 1 or os.environ.get("BO_FORCE_COLLECTIVES") == "1"
     if backend != "nccl":
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -593,13 +596,13 @@ def main():
         print(json.dumps(run_c1(dev)), flush=True)
         return
     if args.iteration:
-        if world > 1:
+        if use_dist:
             dist.init_process_group("nccl" if backend == "nccl" else backend,
                                     **({"device_id": dev} if backend == "nccl" else {}))
         res = run_iteration(args.config, cfg, dev, args, world, rank)
         if rank == 0:
             print(json.dumps(res), flush=True)
-        if world > 1:
+        if use_dist:
             dist.destroy_process_group()
         return
     if args.fit or args.fit_demo:
@@ -608,7 +611,7 @@ def main():
         print(json.dumps(run_fit_demo(args.fit_demo, dev) if args.fit_demo else run_fit(cfg, args.config, dev)),
               flush=True)
         return
-    if world > 1:
+    if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -653,7 +656,7 @@ def main():
     # one all_gather of P * q * 16 bytes
     # (one shard: the record block lives in pinned host memory and the merge kernel writes the
     # selection straight into it -- no device-to-host copy launch per step)
-    rec = torch.empty(2 * q, dtype=torch.float64, device=dev) if world > 1 or args.acq == "hvi" \
+    rec = torch.empty(2 * q, dtype=torch.float64, device=dev) if use_dist or args.acq == "hvi" \
         else torch.empty(2 * q, dtype=torch.float64).pin_memory()
     rec_np = rec.numpy() if rec.device.type == "cpu" else None
     gath = torch.empty(world * 2 * q, dtype=torch.float64, device=dev)
@@ -714,7 +717,7 @@ def main():
             step_hvi()
         else:
             run()
-        if world > 1:
+        if use_dist:
             if backend == "nccl":
                 dist.all_gather_into_tensor(gath, rec)
                 g = gath.view(world, 2 * q).cpu()
@@ -735,7 +738,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     graphed = run is not predict
     if not graphed:
@@ -744,8 +747,11 @@ def main():
     for _ in range(args.steps):
         sel = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
+    # this rank's own fused top-q (before the exchange): what its standalone selection must match
+    local_sel = rec.cpu()[q:].view(torch.int64).numpy() if use_dist else np.asarray(sel[1])
+    local_sel = local_sel[local_sel >= 0]
     dt = time.perf_counter() - t0
     import ctypes
     kms, nl = ctypes.c_double(), ctypes.c_int()
@@ -763,7 +769,7 @@ def main():
         # all_reduce (RCCL) -- outside the timed region, reported beside the selection
         from bayesopt_smart_amd.distributed import front_hypervolume
         hv_front = front_hypervolume(front_y, ref_pt, device=dev)
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([t_step, kms.value / max(nl.value, 1)], dtype=torch.float64,
                           device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -789,6 +795,11 @@ def main():
         pmc_key = args.config if args.mode == ("fp32" if args.config == "C5" else "auto") \
             else f"{args.config}-{args.mode}"
         traffic, traffic_src = pmc_traffic(pmc_key) if args.acq == "sum_ucb" else (None, None)
+        if world > 1 and traffic is not None:
+            # the committed PMC summaries are single-GPU runs over the whole candidate set: not
+            # this rank's per-launch traffic
+            traffic, traffic_src = None, (f"not measured per rank: {traffic_src} is a single-GPU "
+                                          f"summary of the whole candidate set")
         res = {
             "metric": metric,
             "value": total / t_step,
@@ -843,7 +854,7 @@ def main():
                                  "hbm_frac": hb / (hms * 1e-3) / 1e9 / 8000.0}
         if args.acq == "sum_ucb" and q <= 16:
             res["select_standalone"] = standalone_select(lib, bo, out["acq"], cands, offset, per_rank, xd,
-                                                         q, dev, sel[1])
+                                                         q, dev, local_sel)
         if world == 1 and not args.no_cpu_baseline and args.acq == "sum_ucb":
             if cand[0] == "grid":
                 side = cand[2]
@@ -870,8 +881,11 @@ def main():
                 res["cpu_selected"] = [int(i) for i in cpu_sel]
             else:
                 res["selection_matches_cpu"] = None   # sample shorter than the shard
+        if use_dist:
+            res["collectives"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                                  "exchange": "all_gather_into_tensor of the 16-B top-q records per step"}
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 3
+#define BO_ABI_VERSION 4
 #define BO_MAX_OBJ 8      /* objectives per call                              */
 #define BO_MAX_DIM 8      /* input dimensions                                 */
 #define BO_MAX_TOPQ 48    /* batch size of the fused top-q selection          */
@@ -258,13 +258,23 @@ int bo_hypervolume_improvement_exact(double* acq, const double* ucb, int64_t ld,
  * ---------------------------------------------------------------------------------- */
 
 /* invert_k  bayesopt/numba_kernels.py:370-403: out[o] = inv(K[o][:N,:N] + 1e-6 I) (the
- * reference's LAPACK gesv with the identity): a blocked Cholesky when K is symmetric, the blocked
- * LU with partial pivoting (getrf's row choice) + getrs when the Cholesky fails or K is not
- * symmetric.  kernel_matrix device [n_obj][ld][ld];
+ * reference's LAPACK gesv with the identity): a blocked Cholesky when K is symmetric, followed
+ * by one Newton step X + X (I - (K + 1e-6 I) X) on the matrix cores (the residual of gesv's
+ * backward-stable solves), or the blocked LU with partial pivoting (getrf's row choice) + getrs
+ * when the Cholesky fails or K is not symmetric.  kernel_matrix device [n_obj][ld][ld];
  * out device [n_obj][n][n]. Returns BO_ERR_SINGULAR on an exactly singular pivot.
  * Synchronous (the status depends on the factorisation). */
 int bo_invert_k(double* out, const double* kernel_matrix, int64_t ld, int32_t n_obj, int64_t n,
                 void* workspace, size_t workspace_bytes, void* stream);
+/* bo_invert_k_jitter with per-objective path control and report (ABI 4).  lu_hint (host
+ * [n_obj], may be NULL): when EVERY objective's entry is non-zero the Cholesky attempt is skipped
+ * and all of them go straight to the blocked LU -- the caller's knowledge that the previous
+ * iteration's Cholesky failed for them (a drop-in loop at Powell-fitted length scales, where
+ * cond(K + 1e-6 I) > 1e16).  The result is the LU path's either way.  path_out
+ * (host [n_obj], may be NULL): 0 Cholesky (+ Newton step), 1 blocked LU, 2 Gauss-Jordan. */
+int bo_invert_k_ex(double* out, const double* kernel_matrix, int64_t ld, int32_t n_obj, int64_t n,
+                   double jitter, const int32_t* lu_hint, int32_t* path_out, void* workspace,
+                   size_t workspace_bytes, void* stream);
 /* Per-objective counts of the paths bo_invert_k took since the library was loaded (process-wide,
  * host counters): counts[0] Cholesky, [1] blocked LU (Cholesky failed or K not symmetric;
  * N <= 2048), [2] Gauss-Jordan (the same above N = 2048).  Diagnostics for the fallback's
@@ -277,8 +287,10 @@ int bo_invert_k_jitter(double* out, const double* kernel_matrix, int64_t ld, int
 size_t bo_invert_k_workspace_size(int32_t n_obj, int64_t n);
 /* Process-wide counts of the factorisation schedules bo_invert_k / bo_compute_mll* ran:
  * counts[0] the persistent launch (one task-queue kernel: panels and trailing-update tiles hand
- * off through flags), [1] one launch per 32-column step (N > 4064, or BO_FIT_PATH=launches),
- * [2] persistent launches that gave up a wait (bounded spin) and were rerun step by step. */
+ * off through flags), [1] one launch per 32-column step (N > 1536 by default -- more than 48
+ * column blocks of 32; the environment variable BO_FIT_PERSIST_MAX_NBT sets that block count --
+ * or BO_FIT_PATH=launches), [2] persistent launches that gave up a wait (bounded spin) and were
+ * rerun step by step. */
 int bo_fit_path_counts(int64_t* counts);
 
 /* compute_mll  bayesopt/numba_kernels.py:152-235 (Gram rebuilt into kernel_matrix first, as
