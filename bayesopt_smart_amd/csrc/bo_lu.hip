@@ -19,13 +19,17 @@
 //     pairs, by ballots over 32 lanes) that every later consumer reads;
 //   * update (strips > k): step k-1 applied to each strip by its own workgroup (lookahead: the
 //     panel of step k needs only its own strip).
-// The L columns keep the row order of their own step (later swaps are not applied to them:
-// LAPACK's laswp on the left columns), so the solve interleaves the swaps with the forward
-// substitution exactly as the elimination applied them.  Solve (one launch, one workgroup per
-// strip of the identity and objective, no inter-workgroup dependency): W = e_strip; per step s:
-// the step's permutation record (prefetched one step ahead), W_s = L11^-1 W_s, W_below -= L21 W_s;
-// then per step from the last: W_s = U_ss^-1 W_s, W_above -= U_above,s W_s.  W's rows are
-// out[:, strip].
+// The L columns keep the row order of their own step during the factorisation.  After the last
+// step, lu_finalize_kernel applies the later interchanges to them (LAPACK's laswp on the left
+// columns: P A = L U), composes the permutation (P e_c = e at row sinv[c]) and inverts each step's
+// 16 x 16 diagonal blocks L11 and U11.  Solve (lu_solve_mfma_kernel, N <= 1024: one launch, one
+// workgroup per 16-column strip of the identity and objective, no inter-workgroup dependency):
+// W = P e_strip in MFMA accumulator layout; per step s its owner wave applies the inverted
+// diagonal block (4 MFMAs) and publishes T = W_s, then every wave updates its live blocks,
+// W_b -= A[b, s] T (4 MFMAs per block), forward with L then backward with U.  Above N = 1024
+// (lu_solve_kernel): the round-4 solve on the unpermuted factors -- W = e_strip; per step s: the
+// step's permutation record, W_s = L11^-1 W_s by substitution, W_below -= L21 W_s; then per step
+// from the last: W_s = U_ss^-1 W_s, W_above -= U_above,s W_s.  W's rows are out[:, strip].
 //
 // Round 2 ran one Gauss-Jordan launch per pivot (N launches, ~105 ms at N = 2048); round 3's
 // version of this file (one objective per launch sequence, the permutation rebuilt serially by
@@ -35,6 +39,7 @@
 #include "bo_common.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -84,6 +89,8 @@ struct LuGeo {
 struct LuBatch {                // one factorisation per slot (the objectives whose Cholesky failed)
   double* A[BO_MAX_OBJ];
   int* prec[BO_MAX_OBJ];        // nbs permutation records
+  int* sinv[BO_MAX_OBJ];        // [n_p] P's column c is e at row sinv[c] (lu_finalize_kernel)
+  double* tinv[BO_MAX_OBJ];     // [nbs][2][16][16] inverses of each step's L11 and U11, row-major
   const double* km[BO_MAX_OBJ];
   double* out[BO_MAX_OBJ];
   int* status;                  // [slot]: 1 = an exactly zero (or NaN) pivot
@@ -118,10 +125,12 @@ struct StripLds {
   int m;                        // its length
   double T[LB][LB + 1];         // the 16 x 16 block being solved
   double L11[LB][LB + 1];       // the step's diagonal block (L unit lower / U upper)
-  double cand[2][LW][LB];       // panel: each wave's best row, by column parity
+  alignas(16) double cand[2][LW][LB];   // panel: each wave's best row, by column parity
   unsigned long long ck[2][LW]; //        its pivot key
   int cr[2][LW];                //        its row index
-  double grow[2][LB];           //        row j of the column
+  double crp[2][LW];            //        1 / its entry in the column (the pivot's reciprocal)
+  alignas(16) double grow[2][LB];       //        row j of the column
+  double grp[2];                //        1 / its entry
   int piv[LB];                  //        the step's pivot rows
   short smap[LT * LRMAX];          // row -> its slot as a source of the permutation (-1: none)
   short pmap[LT * LRMAX];          // row -> its slot as a destination
@@ -407,6 +416,11 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
       LU_CSTAMP(k, j, 0);
       unsigned long long bk = 0ull;
       int brow = 0x7fffffff;
+      // every row's reciprocal (getf2 scales by 1 / pivot), issued before the wave reduction so
+      // that the division's latency overlaps it instead of following it
+      double rcp[LR];
+#pragma unroll
+      for (int r = 0; r < LR; ++r) rcp[r] = 1.0 / w[r][0];
 #pragma unroll
       for (int r = 0; r < LR; ++r) {
         const long long row = own_row(base, r);
@@ -417,11 +431,13 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
       int wrow;
       piv_wave_best(bk, brow, wk, wrow);
       LU_CSTAMP(k, j, 1);
+      // the wave's pivot candidate row and its reciprocal
 #pragma unroll
       for (int r = 0; r < LR; ++r)
-        if (wk != 0ull && own_row(base, r) == wrow) {                  // the wave's pivot candidate row
+        if (wk != 0ull && own_row(base, r) == wrow) {
 #pragma unroll
-          for (int c = 0; c < LB; ++c) L.cand[bf][wave][c] = w[r][c];
+          for (int c = 0; c < LB; c += 2) *(d2*)&L.cand[bf][wave][c] = (d2){w[r][c], w[r][c + 1]};
+          L.crp[bf][wave] = rcp[r];
         }
       if (lane == 0) {
         L.ck[bf][wave] = wk;
@@ -431,29 +447,42 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
       for (int r = 0; r < LR; ++r)
         if (own_row(base, r) == g0) {
 #pragma unroll
-          for (int c = 0; c < LB; ++c) L.grow[bf][c] = w[r][c];
+          for (int c = 0; c < LB; c += 2) *(d2*)&L.grow[bf][c] = (d2){w[r][c], w[r][c + 1]};
+          L.grp[bf] = rcp[r];
         }
       __syncthreads();
       LU_CSTAMP(k, j, 2);
       unsigned long long kk[LW];
-      int rr[LW];
+      int rr[LW], ww[LW];
 #pragma unroll
-      for (int u = 0; u < LW; ++u) { kk[u] = L.ck[bf][u]; rr[u] = L.cr[bf][u]; }
-      unsigned long long pk = kk[0];
-      int p = rr[0], pw = 0;
+      for (int u = 0; u < LW; ++u) { kk[u] = L.ck[bf][u]; rr[u] = L.cr[bf][u]; ww[u] = u; }
+      // the workgroup's pivot: a 3-level tree over the 8 wave candidates (depth 3, not 7)
 #pragma unroll
-      for (int u = 1; u < LW; ++u) {
-        const bool t = piv_before(kk[u], rr[u], pk, p);
-        pk = t ? kk[u] : pk;
-        p = t ? rr[u] : p;
-        pw = t ? u : pw;
-      }
+      for (int h = LW / 2; h >= 1; h >>= 1)
+#pragma unroll
+        for (int u = 0; u < h; ++u) {
+          const bool t = piv_before(kk[u + h], rr[u + h], kk[u], rr[u]);
+          kk[u] = t ? kk[u + h] : kk[u];
+          rr[u] = t ? rr[u + h] : rr[u];
+          ww[u] = t ? ww[u + h] : ww[u];
+        }
+      const unsigned long long pk = kk[0];
+      int p = rr[0], pw = ww[0];
       // pk - 1 = bits of |pivot|: a zero (or NaN-only) column is singular
       const bool zero = pk <= 1ull;
       if (zero) { singular = true; p = (int)g0; pw = -1; }           // zero / NaN column: no swap
       const double* prow = pw >= 0 ? L.cand[bf][pw] : L.grow[bf];
       if (tid == 0) L.piv[j] = p;
-      const double rp = 1.0 / prow[0];
+      // the pivot row in registers first: every LDS read in flight at once (a read per updated
+      // column inside the branch chain below serialised 15 LDS round trips per column)
+      double pr[LB];
+#pragma unroll
+      for (int c = 0; c < LB; c += 2) {
+        const d2 v = *(const d2*)(prow + c);
+        pr[c] = v.x;
+        pr[c + 1] = v.y;
+      }
+      const double rp = pw >= 0 ? L.crp[bf][pw] : L.grp[bf];
       const int live = LB - j;                        // rotated columns 1 .. live - 1 are updated
       double l[LR];
       bool act[LR];
@@ -462,10 +491,14 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
         const long long row = own_row(base, r);
         if (row == g0) {
 #pragma unroll
-          for (int c = 0; c < LB; ++c) w[r][c] = prow[c];
+          for (int c = 0; c < LB; ++c) w[r][c] = pr[c];
         } else if (row == p) {
 #pragma unroll
-          for (int c = 0; c < LB; ++c) w[r][c] = L.grow[bf][c];
+          for (int c = 0; c < LB; c += 2) {
+            const d2 v = *(const d2*)&L.grow[bf][c];
+            w[r][c] = v.x;
+            w[r][c + 1] = v.y;
+          }
         }
         act[r] = row > g0 && row < g.n_p;
         l[r] = w[r][0] * rp;
@@ -474,10 +507,9 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
 #pragma unroll
       for (int c = 1; c < LB; ++c)
         if (c < live) {
-          const double pc = prow[c];                  // one LDS broadcast serves the thread's rows
 #pragma unroll
           for (int r = 0; r < LR; ++r)
-            if (act[r]) w[r][c] = __builtin_fma(-l[r], pc, w[r][c]);
+            if (act[r]) w[r][c] = __builtin_fma(-l[r], pr[c], w[r][c]);
         }
 #pragma unroll
       for (int r = 0; r < LR; ++r) {
@@ -503,9 +535,248 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
   }
 }
 
+// ----------------------------------------------------------------------- finalize (laswp)
+// After the last step: getrf's form P A = L U.  Workgroup s < nbs applies the row interchanges of
+// the steps after s to strip s's L columns (LAPACK's laswp on the left columns): wave 0 composes
+// the records s+1 .. nbs-1 into the gather map g (position i <- stored row g(i)) in LDS, then the
+// strip's rows below its diagonal block are gathered in place (every load of the workgroup before
+// any store; the workgroups own disjoint columns).  Workgroup nbs composes every record into
+// sigma (position i <- original row sigma(i)) and stores sinv = sigma^-1 (column c of P is e at
+// row sinv(c)) and the reciprocals of U's diagonal for the solve.
+__device__ void compose_records(int* __restrict__ gmap, const int* __restrict__ prec, int t0, int t1, int n_p) {
+  const int lane = threadIdx.x & 63;
+  for (int i = lane; i < n_p; i += 64) gmap[i] = i;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int m = 0, pos = 0, src = 0;
+  if (t0 < t1 && lane < 32) get_perm(prec + (long long)t0 * PREC, m, pos, src);
+  for (int t = t0; t < t1; ++t) {
+    const int cm = m, cp = pos, cs = src;
+    if (t + 1 < t1 && lane < 32) get_perm(prec + (long long)(t + 1) * PREC, m, pos, src);   // next, in flight
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int v = lane < cm ? gmap[cs] : 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < cm) gmap[cp] = v;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Inverses of strip s's diagonal blocks (final after step s; later interchanges never reach rows
+// < 16 (s + 1)) by substitution on the identity, one column per lane: wave 1 the unit lower L11,
+// wave 2 the upper U11.  The solve then applies each step's triangle as four MFMAs.  (Inverted
+// diagonal blocks are rocBLAS trsm's method; against substitution they moved the residual
+// |A X - I| by 1.0-1.8x in a numpy model at cond 1e4..2e19, scripts/lu_invdiag_model.py.)
+__device__ void diag_block_inverses(const double* __restrict__ A, long long Na, int s, double* __restrict__ tinv) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((wave != 1 && wave != 2) || lane >= LB) return;
+  const long long cs = (long long)LB * s;
+  const int t = lane;
+  double x[LB];
+  if (wave == 1) {                                     // L11^-1 (unit lower)
+#pragma unroll
+    for (int i = 0; i < LB; ++i) x[i] = i == t ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 1; i < LB; ++i)
+#pragma unroll
+      for (int m = 0; m < i; ++m) x[i] = __builtin_fma(-A[(cs + m) * Na + cs + i], x[m], x[i]);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) tinv[(long long)s * 512 + i * LB + t] = x[i];
+  } else {                                             // U11^-1 (upper, with its diagonal)
+#pragma unroll
+    for (int i = 0; i < LB; ++i) x[i] = i == t ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = LB - 1; i >= 0; --i) {
+#pragma unroll
+      for (int m = i + 1; m < LB; ++m) x[i] = __builtin_fma(-A[(cs + m) * Na + cs + i], x[m], x[i]);
+      x[i] = x[i] / A[(cs + i) * Na + cs + i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) tinv[(long long)s * 512 + 256 + i * LB + t] = x[i];
+  }
+}
+
+template <int LR>
+__global__ __launch_bounds__(LT) void lu_finalize_kernel(LuBatch bt, LuGeo g) {
+  __shared__ int gmap[LT * LRMAX];
+  const int s = blockIdx.x, slot = blockIdx.y, tid = threadIdx.x;
+  double* __restrict__ A = bt.A[slot];
+  const int* __restrict__ prec = bt.prec[slot];
+  if (s == g.nbs) {
+    if (tid < 64) compose_records(gmap, prec, 0, g.nbs, g.n_p);
+    __syncthreads();
+    for (int i = tid; i < g.n_p; i += LT) bt.sinv[slot][gmap[i]] = i;
+    return;
+  }
+  diag_block_inverses(A, g.Na, s, bt.tinv[slot]);
+  if (s + 1 >= g.nbs) return;                          // the last strip: no later interchanges
+  if (tid < 64) compose_records(gmap, prec, s + 1, g.nbs, g.n_p);
+  __syncthreads();
+  const long long c0 = (long long)LB * s;
+  const int base = LB * (s + 1);
+  double w[LR][LB];
+#pragma unroll
+  for (int r = 0; r < LR; ++r) {
+    const long long row = own_row(base, r);
+    const long long src = row < g.n_p ? gmap[row] : base;
+#pragma unroll
+    for (int c = 0; c < LB; ++c) w[r][c] = A[(c0 + c) * g.Na + src];
+  }
+  __syncthreads();                                     // every gather load before any store
+#pragma unroll
+  for (int r = 0; r < LR; ++r) {
+    const long long row = own_row(base, r);
+    if (row >= g.n_p || gmap[row] == row) continue;
+#pragma unroll
+    for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + row] = w[r][c];
+  }
+}
+
 // ------------------------------------------------------------------------------ solve
-// out[:, 16 strip .. 16 strip + 15] = inv(A) e_col: forward with the interleaved permutations
-// and L, backward with U.  One workgroup per strip of the identity (grid x) and slot (grid y).
+// getrs with the identity on the matrix cores: out[:, 16 strip + c] = U^-1 L^-1 P e_{16 strip + c}
+// (P e_col = e at row sinv(col)).  One 512-thread workgroup per strip of the identity (grid x) and
+// slot (grid y), no inter-workgroup dependency.  W (n_p x 16) lives in v_mfma_f64_16x16x4_f64
+// accumulator layout: 16-row block b is wave b % 8's accumulator b / 8, lane (li, lg) holding
+// W[16 b + lg + 4 i][li].  Per step s the block's owner wave solves the 16 x 16 triangle (16 lanes,
+// one column each, the chain in registers; L11 / U_ss staged in LDS), publishes T = W_s in LDS, and
+// after one barrier every wave applies the rank-16 update to its live blocks: W_b -= A[b rows, s
+// columns] T, four MFMAs per block with the A operand read straight from the column-major factors
+// (16 consecutive rows per column: coalesced).  Forward from the first block holding a non-zero of
+// P e (the blocks above it stay zero), backward over every block.  The previous version held one
+// row per thread and read T as LDS broadcasts (256 per row per step: ~1.7 us of LDS per step at
+// N = 512) with the step's permutation applied through LDS (three barriers per step).
+__device__ __forceinline__ void acc_fence(d4& x) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(x));
+}
+
+// One direction of the solve.  Step s: its owner wave (s & 7) applies the step's triangle to its
+// block, T = tinv_s W_s (four MFMAs: the f64 accumulator layout -- lane (li, lg) holds rows
+// lg + 4 i of column li -- is exactly the B-operand layout of the four k-steps), and publishes T
+// in LDS; after one barrier every wave subtracts A[rows of its live blocks, columns of s] T.  The
+// triangle's A operand (row li, columns 4 ks + lg of the inverse) is prefetched one owned step
+// ahead, the update's before the barrier.
+template <bool FWD, int NBW>
+__device__ __forceinline__ void solve_phase(double (&Ts)[2][LB][LB + 1], d4 (&acc)[NBW], const double* __restrict__ A,
+                                            const double* __restrict__ tinv, long long Na, int nbs, int first,
+                                            int& par) {
+  constexpr int PF = NBW <= 4 ? NBW : 2;     // blocks whose A operand is prefetched a step ahead
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  // the update's A operand for step st (rows of this wave's live blocks, columns of st): issued one
+  // step ahead, so that its L2 latency overlaps the previous step
+  auto av_load = [&](int st, double (&v)[PF][4]) {
+    const long long cst = (long long)LB * st;
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int b = 8 * q + wave;
+      const bool live = b < nbs && (FWD ? b > st : b < st);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        v[q][ks] = live ? -A[(cst + 4 * ks + lg) * Na + (long long)LB * b + li] : 0.0;
+    }
+  };
+  auto tri_load = [&](int st, double (&v)[4]) {
+    const double* ti = tinv + (long long)st * 512 + (FWD ? 0 : 256) + li * LB + lg;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) v[ks] = ti[4 * ks];
+  };
+  const int s_beg = FWD ? first : nbs - 1;
+  int my = FWD ? s_beg + ((wave - s_beg) & 7) : s_beg - ((s_beg - wave) & 7);
+  double tri[4] = {0.0, 0.0, 0.0, 0.0};
+  if (FWD ? my < nbs : my >= 0) tri_load(my, tri);
+  double avn[PF][4];
+  av_load(s_beg, avn);
+  // steps in groups of 8: step s = 8 gq + w8 is wave w8's block gq, so the owner's accumulator
+  // index is static (a runtime index put acc in scratch)
+#pragma unroll
+  for (int gi = 0; gi < NBW; ++gi) {
+    const int gq = FWD ? gi : NBW - 1 - gi;
+#pragma unroll 1
+    for (int u = 0; u < 8; ++u) {
+      const int w8 = FWD ? u : 7 - u;
+      const int s = 8 * gq + w8;
+      if (s >= nbs || (FWD && s < first)) continue;            // uniform
+      const long long cs = (long long)LB * s;
+      double av[PF][4];
+#pragma unroll
+      for (int q = 0; q < PF; ++q)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) av[q][ks] = avn[q][ks];
+      const int sn = FWD ? s + 1 : s - 1;
+      if (FWD ? sn < nbs : sn >= 0) av_load(sn, avn);
+      if (wave == w8) {
+        acc_fence(acc[gq]);
+        d4 tq = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) tq = __builtin_amdgcn_mfma_f64_16x16x4f64(tri[ks], acc[gq][ks], tq, 0, 0, 0);
+        acc_fence(tq);
+        acc[gq] = tq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ts[par][lg + 4 * i][li] = tq[i];
+        my = FWD ? s + 8 : s - 8;
+        if (FWD ? my < nbs : my >= 0) tri_load(my, tri);
+      }
+      __syncthreads();
+      double tb[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) tb[ks] = Ts[par][4 * ks + lg][li];
+#pragma unroll
+      for (int q = 0; q < NBW; ++q) {
+        const int b = 8 * q + wave;
+        if (b >= nbs || (FWD ? b <= s : b >= s)) continue;      // wave-uniform
+        double a2[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          a2[ks] = q < PF ? av[q < PF ? q : 0][ks] : -A[(cs + 4 * ks + lg) * Na + (long long)LB * b + li];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[ks], tb[ks], acc[q], 0, 0, 0);
+      }
+      par ^= 1;
+    }
+  }
+}
+
+template <int NBW>
+__global__ __launch_bounds__(LT) void lu_solve_mfma_kernel(LuBatch bt, LuGeo g) {
+  __shared__ double Ts[2][LB][LB + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int strip = blockIdx.x, slot = blockIdx.y;
+  const double* __restrict__ A = bt.A[slot];
+  const double* __restrict__ tinv = bt.tinv[slot];
+  double* __restrict__ out = bt.out[slot];
+  // W = P e_strip
+  const int srow = bt.sinv[slot][LB * strip + li];
+  d4 acc[NBW];
+#pragma unroll
+  for (int q = 0; q < NBW; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[q][i] = (LB * (8 * q + wave) + lg + 4 * i == srow) ? 1.0 : 0.0;
+  // the first block with a non-zero of P e_strip: the forward steps before it change nothing
+  int first = srow / LB;
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) first = min(first, __shfl_xor(first, m, 64));
+  first = __builtin_amdgcn_readfirstlane(first);
+  int par = 0;
+  solve_phase<true, NBW>(Ts, acc, A, tinv, g.Na, g.nbs, first, par);
+  solve_phase<false, NBW>(Ts, acc, A, tinv, g.Na, g.nbs, 0, par);
+#pragma unroll
+  for (int q = 0; q < NBW; ++q) {
+    const int b = 8 * q + wave;
+    if (b >= g.nbs) continue;
+    acc_fence(acc[q]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long row = (long long)LB * b + lg + 4 * i, col = (long long)LB * strip + li;
+      if (row < g.n && col < g.n) out[row * g.n + col] = acc[q][i];
+    }
+  }
+}
+
+// (round 4) out[:, 16 strip .. 16 strip + 15] = inv(A) e_col: forward with the interleaved
+// permutations and L, backward with U.  One workgroup per strip of the identity (grid x) and slot
+// (grid y).  Kept for A/B measurements (BO_LU_SOLVE=rows).
 template <int LR>
 __global__ __launch_bounds__(LT) void lu_solve_kernel(LuBatch bt, LuGeo g) {
   __shared__ StripLds L;
@@ -638,7 +909,17 @@ LuGeo make_lu_geo(int n) {
 }
 
 size_t slot_bytes(const LuGeo& g) {
-  return a256((size_t)g.Na * g.n_p * sizeof(double)) + a256((size_t)g.nbs * PREC * sizeof(int));
+  return a256((size_t)g.Na * g.n_p * sizeof(double)) + a256((size_t)g.nbs * PREC * sizeof(int)) +
+         a256((size_t)g.n_p * sizeof(int)) + a256((size_t)g.nbs * 512 * sizeof(double));
+}
+
+// BO_LU_SOLVE=rows: the round-4 solve (interleaved permutations, one row per thread) for A/B
+bool lu_solve_rows() {
+  static const int v = [] {
+    const char* e = getenv("BO_LU_SOLVE");
+    return (e && strcmp(e, "rows") == 0) ? 1 : 0;
+  }();
+  return v != 0;
 }
 
 }  // namespace
@@ -664,6 +945,8 @@ int bo_lu_inverse(double* const* out, const double* const* km, int n_lu, int64_t
   for (int b = 0; b < n_lu; ++b) {
     bt.A[b] = (double*)w;
     bt.prec[b] = (int*)(w + a256((size_t)g.Na * g.n_p * sizeof(double)));
+    bt.sinv[b] = (int*)((char*)bt.prec[b] + a256((size_t)g.nbs * PREC * sizeof(int)));
+    bt.tinv[b] = (double*)((char*)bt.sinv[b] + a256((size_t)g.n_p * sizeof(int)));
     bt.km[b] = km[b];
     bt.out[b] = out[b];
     w += slot_bytes(g);
@@ -675,12 +958,24 @@ int bo_lu_inverse(double* const* out, const double* const* km, int n_lu, int64_t
   // rows per thread: the fewest that hold N_p (at N = 512 one row, so no predicated-off rows)
   const int lr = (g.n_p + LT - 1) / LT;
   auto step = lr == 1 ? lu_step_kernel<1> : lr == 2 ? lu_step_kernel<2> : lu_step_kernel<4>;
-  auto solve = lr == 1 ? lu_solve_kernel<1> : lr == 2 ? lu_solve_kernel<2> : lu_solve_kernel<4>;
   for (int k = 0; k < g.nbs; ++k) {
     const int blocks = k > 0 ? g.nbs - k : 1;      // the panel + the strips right of it
     hipLaunchKernelGGL(step, dim3(blocks, n_lu), dim3(LT), 0, s, bt, g, k);
   }
-  hipLaunchKernelGGL(solve, dim3(g.nbs, n_lu), dim3(LT), 0, s, bt, g);
+  const int nbw = (g.nbs + 7) / 8;
+  if (lu_solve_rows() || nbw > 8) {
+    // N > 1024 (the 16-accumulator solve spills) or BO_LU_SOLVE=rows: the row-per-thread solve
+    auto solve = lr == 1 ? lu_solve_kernel<1> : lr == 2 ? lu_solve_kernel<2> : lu_solve_kernel<4>;
+    hipLaunchKernelGGL(solve, dim3(g.nbs, n_lu), dim3(LT), 0, s, bt, g);
+  } else {
+    // laswp of the L columns, the permutation and the diagonal blocks' inverses, then the
+    // matrix-core solve
+    auto fin = lr == 1 ? lu_finalize_kernel<1> : lr == 2 ? lu_finalize_kernel<2> : lu_finalize_kernel<4>;
+    hipLaunchKernelGGL(fin, dim3(g.nbs + 1, n_lu), dim3(LT), 0, s, bt, g);
+    auto solve = nbw <= 1 ? lu_solve_mfma_kernel<1> : nbw <= 2 ? lu_solve_mfma_kernel<2> :
+                 nbw <= 4 ? lu_solve_mfma_kernel<4> : lu_solve_mfma_kernel<8>;
+    hipLaunchKernelGGL(solve, dim3(g.nbs, n_lu), dim3(LT), 0, s, bt, g);
+  }
   BO_CHECK_HIP(hipGetLastError());
   int hs[BO_MAX_OBJ];
   BO_CHECK_HIP(hipMemcpyAsync(hs, bt.status, sizeof(int) * BO_MAX_OBJ, hipMemcpyDeviceToHost, s));

@@ -16,7 +16,7 @@ dev = torch.device("cuda", 0)
 xd = torch.tensor(x, device=dev)
 km = torch.zeros((n_obj, n, n), dtype=torch.float64, device=dev)
 bo.kernels.update_k(km, xd, 0, n, pv, np.full(n_obj, ls_fit))
-g = lambda: bo.kernels.invert_k(n, km)
+g = lambda: bo.kernels.invert_k(n, km, lu_hint=[True] * n_obj)   # straight to the LU path
 before = bo._lib.fit_path_counts()
 g(); torch.cuda.synchronize()
 print("fit paths after one call:", {k: v - before.get(k, 0) for k, v in bo._lib.fit_path_counts().items()})

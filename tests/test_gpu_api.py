@@ -321,7 +321,7 @@ def test_demo_trajectory_replay_each_iteration(bo, it):
             assert abs(acq[sel[t]] - rval[t]) <= 2 * tt, (it, t)
 
 
-@pytest.mark.parametrize("n", [512, 2048])
+@pytest.mark.parametrize("n", [512, 518, 1000, 2048])
 def test_invert_k_lu_path_matches_lapack(bo, n):
     """invert_k's blocked LU path (bo_lu.hip: getrf partial pivoting + getrs with the identity,
     numba_kernels.py:401) at the C3 and C5 N: objective 0's K is made non-symmetric (the Cholesky
