@@ -49,8 +49,7 @@ namespace {
 constexpr int LB = 16;          // strip width
 constexpr int LT = 512;         // threads per strip workgroup (256 VGPRs: the rows stay in registers)
 constexpr int LRMAX = 4;        // rows per thread (kernels templated on LR = 1, 2, 4 by N_p): N_p <= 2048
-constexpr int LW = LT / 64;     // waves per workgroup (solve / finalize kernels)
-constexpr int LWMAX = 16;       // waves of the step kernel's one-row-per-thread form (N_p <= 1024)
+constexpr int LW = LT / 64;     // waves per workgroup
 constexpr int PREC = 72;        // ints per step's permutation record: [0] m, [8, 40) pos, [40, 72) src
 
 // Diagnostic build (BO_BUILD_VARIANT=DEF_FIT_TIMING): the panel workgroup of each step launch
@@ -126,10 +125,10 @@ struct StripLds {
   int m;                        // its length
   double T[LB][LB + 1];         // the 16 x 16 block being solved
   double L11[LB][LB + 1];       // the step's diagonal block (L unit lower / U upper)
-  alignas(16) double cand[2][LWMAX][LB];   // panel: each wave's best row, by column parity
-  unsigned long long ck[2][LWMAX]; //        its pivot key
-  int cr[2][LWMAX];                //        its row index
-  double crp[2][LWMAX];            //        1 / its entry in the column (the pivot's reciprocal)
+  alignas(16) double cand[2][LW][LB];   // panel: each wave's best row, by column parity
+  unsigned long long ck[2][LW]; //        its pivot key
+  int cr[2][LW];                //        its row index
+  double crp[2][LW];            //        1 / its entry in the column (the pivot's reciprocal)
   alignas(16) double grow[2][LB];       //        row j of the column
   double grp[2];                //        1 / its entry
   int piv[LB];                  //        the step's pivot rows
@@ -138,15 +137,11 @@ struct StripLds {
 };
 
 __device__ __forceinline__ void init_maps(StripLds& L) {
-  for (int i = threadIdx.x; i < LT * LRMAX; i += blockDim.x) { L.smap[i] = -1; L.pmap[i] = -1; }
+  for (int i = threadIdx.x; i < LT * LRMAX; i += LT) { L.smap[i] = -1; L.pmap[i] = -1; }
 }
 
 // row `base + t + LT r` of the strip is w[r][*] of thread t
-// the step kernel runs blockDim.x = 64 ceil(N_p / 64) threads (at least 256, at most 1024) with
-// one row per thread up to N_p = 1024, else 512 threads with LR rows each; the other kernels 512
-__device__ __forceinline__ long long own_row(int base, int r) {
-  return (long long)base + threadIdx.x + (long long)blockDim.x * r;
-}
+__device__ __forceinline__ long long own_row(int base, int r) { return (long long)base + threadIdx.x + (long long)LT * r; }
 
 // the permutation record's pairs into LDS (threads 0..31 hold them in registers, loaded earlier),
 // and the row -> slot maps
@@ -381,7 +376,7 @@ __device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const 
 // Launch k: block 0 = panel (strip k), blocks 1.. = strips k + 1 .. (update of step k-1);
 // grid y = the batch slot.
 template <int LR>
-__global__ __launch_bounds__(LR == 1 ? 1024 : LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k) {
+__global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k) {
   __shared__ StripLds L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int slot = blockIdx.y;
@@ -457,19 +452,13 @@ __global__ __launch_bounds__(LR == 1 ? 1024 : LT) void lu_step_kernel(LuBatch bt
         }
       __syncthreads();
       LU_CSTAMP(k, j, 2);
-      constexpr int NWT = LR == 1 ? LWMAX : LW;        // the tree's width (waves beyond blockDim: empty)
-      const int nwv = (int)(blockDim.x >> 6);
-      unsigned long long kk[NWT];
-      int rr[NWT], ww[NWT];
+      unsigned long long kk[LW];
+      int rr[LW], ww[LW];
 #pragma unroll
-      for (int u = 0; u < NWT; ++u) {
-        kk[u] = u < nwv ? L.ck[bf][u] : 0ull;
-        rr[u] = u < nwv ? L.cr[bf][u] : 0x7fffffff;
-        ww[u] = u;
-      }
-      // the workgroup's pivot: a tree over the wave candidates (depth log2 of the waves)
+      for (int u = 0; u < LW; ++u) { kk[u] = L.ck[bf][u]; rr[u] = L.cr[bf][u]; ww[u] = u; }
+      // the workgroup's pivot: a 3-level tree over the 8 wave candidates (depth 3, not 7)
 #pragma unroll
-      for (int h = NWT / 2; h >= 1; h >>= 1)
+      for (int h = LW / 2; h >= 1; h >>= 1)
 #pragma unroll
         for (int u = 0; u < h; ++u) {
           const bool t = piv_before(kk[u + h], rr[u + h], kk[u], rr[u]);
@@ -668,22 +657,10 @@ __device__ __forceinline__ void acc_fence(d4& x) {
 // in LDS; after one barrier every wave subtracts A[rows of its live blocks, columns of s] T.  The
 // triangle's A operand (row li, columns 4 ks + lg of the inverse) is prefetched one owned step
 // ahead, the update's before the barrier.
-// T of solve step t lives in ring slot t % kTR; its flag word holds t + 1 once written.  The owner of
-// the NEXT step updates that step's block first, applies the triangle and publishes the next T at
-// once; the other waves consume T when they get to it (no per-step barrier: the critical path is
-// the chain of owners, ~8 MFMAs and an LDS round trip per step).  A barrier every kTP steps keeps a
-// slot from being rewritten before every wave has read it: between two barriers the owners write
-// at most kTP + 1 slots ahead of the slowest wave, so kTR >= 2 kTP suffices.
-constexpr int kTR = 16, kTP = 8;
-struct SolveRing {
-  double T[kTR][LB][LB + 1];
-  int flag[kTR];
-};
-
 template <bool FWD, int NBW>
-__device__ __forceinline__ void solve_phase(SolveRing& R, d4 (&acc)[NBW], const double* __restrict__ A,
+__device__ __forceinline__ void solve_phase(double (&Ts)[2][LB][LB + 1], d4 (&acc)[NBW], const double* __restrict__ A,
                                             const double* __restrict__ tinv, long long Na, int nbs, int first,
-                                            int& t) {
+                                            int& par) {
   constexpr int PF = NBW <= 4 ? NBW : 2;     // blocks whose A operand is prefetched a step ahead
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
   // the update's A operand for step st (rows of this wave's live blocks, columns of st): issued one
@@ -704,40 +681,14 @@ __device__ __forceinline__ void solve_phase(SolveRing& R, d4 (&acc)[NBW], const 
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) v[ks] = ti[4 * ks];
   };
-  // the owner's triangle on its block: T = tinv W (4 MFMAs; the f64 accumulator layout is the
-  // B-operand layout of the four k-steps), published in slot tt % kTR with flag tt + 1
-  auto triangle = [&](d4& w, const double (&tri)[4], int tt) {
-    acc_fence(w);
-    d4 tq = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) tq = __builtin_amdgcn_mfma_f64_16x16x4f64(tri[ks], w[ks], tq, 0, 0, 0);
-    acc_fence(tq);
-    w = tq;
-    const int sl = tt % kTR;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) R.T[sl][lg + 4 * i][li] = tq[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(&R.flag[sl], tt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
   const int s_beg = FWD ? first : nbs - 1;
   int my = FWD ? s_beg + ((wave - s_beg) & 7) : s_beg - ((s_beg - wave) & 7);
   double tri[4] = {0.0, 0.0, 0.0, 0.0};
   if (FWD ? my < nbs : my >= 0) tri_load(my, tri);
   double avn[PF][4];
   av_load(s_beg, avn);
-  // the phase's first step: its owner applies the triangle to its (complete) block
-  {
-    const int gq0 = s_beg >> 3;
-#pragma unroll
-    for (int q = 0; q < NBW; ++q)
-      if (q == gq0 && wave == (s_beg & 7)) {
-        triangle(acc[q], tri, t);
-        my = FWD ? s_beg + 8 : s_beg - 8;
-        if (FWD ? my < nbs : my >= 0) tri_load(my, tri);
-      }
-  }
-  // steps in groups of 8: step s = 8 gq + w8 is wave w8's block gq, so every accumulator index
-  // below is static (a runtime index put acc in scratch)
+  // steps in groups of 8: step s = 8 gq + w8 is wave w8's block gq, so the owner's accumulator
+  // index is static (a runtime index put acc in scratch)
 #pragma unroll
   for (int gi = 0; gi < NBW; ++gi) {
     const int gq = FWD ? gi : NBW - 1 - gi;
@@ -747,47 +698,33 @@ __device__ __forceinline__ void solve_phase(SolveRing& R, d4 (&acc)[NBW], const 
       const int s = 8 * gq + w8;
       if (s >= nbs || (FWD && s < first)) continue;            // uniform
       const long long cs = (long long)LB * s;
-      const int sl = t % kTR;
-      while (__hip_atomic_load(&R.flag[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t + 1)
-        __builtin_amdgcn_s_sleep(1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      double tb[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) tb[ks] = R.T[sl][4 * ks + lg][li];
       double av[PF][4];
 #pragma unroll
       for (int q = 0; q < PF; ++q)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) av[q][ks] = avn[q][ks];
       const int sn = FWD ? s + 1 : s - 1;
-      const bool has_next = FWD ? sn < nbs : sn >= 0;
-      if (has_next) av_load(sn, avn);
-      // block sn's accumulator index: gq, or the neighbouring group's at the group edge
-      const bool edge = FWD ? w8 == 7 : w8 == 0;
-      const int qn = edge ? (FWD ? gq + 1 : gq - 1) : gq;
-      const bool own_next = has_next && wave == (sn & 7);
-      // the next step's owner: its block first, then its triangle and the next T
-      if (own_next) {
+      if (FWD ? sn < nbs : sn >= 0) av_load(sn, avn);
+      if (wave == w8) {
+        acc_fence(acc[gq]);
+        d4 tq = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < NBW; ++q)
-          if (q == qn) {
-            double a2[4];
+        for (int ks = 0; ks < 4; ++ks) tq = __builtin_amdgcn_mfma_f64_16x16x4f64(tri[ks], acc[gq][ks], tq, 0, 0, 0);
+        acc_fence(tq);
+        acc[gq] = tq;
 #pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-              a2[ks] = q < PF ? av[q < PF ? q : 0][ks] : -A[(cs + 4 * ks + lg) * Na + (long long)LB * sn + li];
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-              acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[ks], tb[ks], acc[q], 0, 0, 0);
-            triangle(acc[q], tri, t + 1);
-            my = FWD ? sn + 8 : sn - 8;
-            if (FWD ? my < nbs : my >= 0) tri_load(my, tri);
-          }
+        for (int i = 0; i < 4; ++i) Ts[par][lg + 4 * i][li] = tq[i];
+        my = FWD ? s + 8 : s - 8;
+        if (FWD ? my < nbs : my >= 0) tri_load(my, tri);
       }
+      __syncthreads();
+      double tb[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) tb[ks] = Ts[par][4 * ks + lg][li];
 #pragma unroll
       for (int q = 0; q < NBW; ++q) {
         const int b = 8 * q + wave;
         if (b >= nbs || (FWD ? b <= s : b >= s)) continue;      // wave-uniform
-        if (own_next && q == qn) continue;
         double a2[4];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
@@ -795,15 +732,14 @@ __device__ __forceinline__ void solve_phase(SolveRing& R, d4 (&acc)[NBW], const 
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[ks], tb[ks], acc[q], 0, 0, 0);
       }
-      ++t;
-      if (t % kTP == 0) __syncthreads();                        // ring slots free again
+      par ^= 1;
     }
   }
 }
 
 template <int NBW>
 __global__ __launch_bounds__(LT) void lu_solve_mfma_kernel(LuBatch bt, LuGeo g) {
-  __shared__ SolveRing R;
+  __shared__ double Ts[2][LB][LB + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lg = lane >> 4;
   const int strip = blockIdx.x, slot = blockIdx.y;
@@ -822,11 +758,9 @@ __global__ __launch_bounds__(LT) void lu_solve_mfma_kernel(LuBatch bt, LuGeo g) 
 #pragma unroll
   for (int m = 1; m < 16; m <<= 1) first = min(first, __shfl_xor(first, m, 64));
   first = __builtin_amdgcn_readfirstlane(first);
-  if (tid < kTR) R.flag[tid] = 0;
-  __syncthreads();
-  int t = 0;
-  solve_phase<true, NBW>(R, acc, A, tinv, g.Na, g.nbs, first, t);
-  solve_phase<false, NBW>(R, acc, A, tinv, g.Na, g.nbs, 0, t);
+  int par = 0;
+  solve_phase<true, NBW>(Ts, acc, A, tinv, g.Na, g.nbs, first, par);
+  solve_phase<false, NBW>(Ts, acc, A, tinv, g.Na, g.nbs, 0, par);
 #pragma unroll
   for (int q = 0; q < NBW; ++q) {
     const int b = 8 * q + wave;
@@ -1021,15 +955,12 @@ int bo_lu_inverse(double* const* out, const double* const* km, int n_lu, int64_t
   BO_CHECK_HIP(hipMemsetAsync(bt.status, 0, sizeof(int) * BO_MAX_OBJ, s));
   const unsigned tiles = (unsigned)((g.n_p + 31) / 32);
   hipLaunchKernelGGL(lu_init_kernel, dim3(tiles, tiles, n_lu), dim3(256), 0, s, bt, g, (long long)ld, jitter);
-  // rows per thread: one up to N_p = 1024 (64 ceil(N_p / 64) threads, at least 256: the C3 loop's
-  // N = 515..548 ran 512 threads x 2 rows at 47.8 us per step), else four on 512 threads
+  // rows per thread: the fewest that hold N_p (at N = 512 one row, so no predicated-off rows)
   const int lr = (g.n_p + LT - 1) / LT;
-  const int nt1 = g.n_p <= 1024 ? ((g.n_p + 63) / 64 * 64 < 256 ? 256 : (g.n_p + 63) / 64 * 64) : LT;
-  auto step = g.n_p <= 1024 ? lu_step_kernel<1> : lu_step_kernel<4>;
-  const int step_threads = g.n_p <= 1024 ? nt1 : LT;
+  auto step = lr == 1 ? lu_step_kernel<1> : lr == 2 ? lu_step_kernel<2> : lu_step_kernel<4>;
   for (int k = 0; k < g.nbs; ++k) {
     const int blocks = k > 0 ? g.nbs - k : 1;      // the panel + the strips right of it
-    hipLaunchKernelGGL(step, dim3(blocks, n_lu), dim3(step_threads), 0, s, bt, g, k);
+    hipLaunchKernelGGL(step, dim3(blocks, n_lu), dim3(LT), 0, s, bt, g, k);
   }
   const int nbw = (g.nbs + 7) / 8;
   if (lu_solve_rows() || nbw > 8) {
