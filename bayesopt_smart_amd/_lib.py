@@ -22,7 +22,7 @@ MAX_TOPQ = 48
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_WORKSPACE, ERR_HIP, ERR_NOT_PD, ERR_SINGULAR = range(7)
 CAND_I64, CAND_F64, CAND_GRID, CAND_SOBOL = 0, 1, 2, 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 MODE_AUTO, MODE_DENSE, MODE_NO_SEPARABLE, MODE_FP32, MODE_F32_FLOOR = 0, 1, 2, 4, 8
 
 c_dbl_p = C.POINTER(C.c_double)
@@ -105,6 +105,16 @@ _SIGS = {
                                  C.POINTER(C.c_int64), C.c_int32, C.c_int64, c_vp, C.c_int64,
                                  C.c_int32, c_vp, c_vp, c_vp, C.c_size_t, c_vp]),
     "bo_select_topq_workspace_size": (C.c_size_t, [C.c_int64, C.c_int32]),
+    "bo_excl_mask_bytes": (C.c_size_t, [C.c_int64]),
+    "bo_excl_mask_workspace_size": (C.c_size_t, [C.c_int64]),
+    "bo_excl_mask_update": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, C.POINTER(C.c_int64),
+                                      C.POINTER(C.c_int64), C.c_int32, C.c_int64, c_vp, C.c_int64,
+                                      C.c_int64, C.c_int32, c_vp, C.c_size_t, c_vp]),
+    "bo_select_topq_masked": (C.c_int, [c_vp, C.c_int64, C.c_int64, c_vp, C.c_int32, c_vp, c_vp, c_vp,
+                                        C.c_size_t, c_vp]),
+    "bo_hvi_select_topq_masked": (C.c_int, [c_vp, c_vp, C.c_int64, C.c_int64, C.c_int32, c_dbl_p, c_dbl_p,
+                                            c_vp, C.c_int64, C.c_int64, c_vp, C.c_int32, c_vp, c_vp, c_vp,
+                                            C.c_size_t, c_vp]),
     "bo_pareto_mask": (C.c_int, [c_vp, C.c_int64, C.c_int32, c_vp, c_vp]),
     "bo_hvi_boxes": (C.c_int, [c_dbl_p, C.c_int64, C.c_int32, c_dbl_p, c_vp, C.c_int64,
                                C.POINTER(C.c_int64)]),

@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .device import F64, Workspace, stream_handle
+from .device import F64, Workspace, require_device, stream_handle
 from .kernels import _Arg, _dev_of, _host_vec
 
 C_i64 = _C.c_int64
@@ -52,18 +52,90 @@ def update_hypervolume_improvement(acquisition_values, ucb):
     a.finish()
 
 
-def select_indices(acquisition_values, cands, evaluated_points, batch_size, dev=None):
+def _grid_args(cands):
+    lo = (C_i64 * 8)(*(list(cands.lo or []) + [0] * (8 - len(cands.lo or []))))
+    sh = (C_i64 * 8)(*(list(cands.shape or []) + [1] * (8 - len(cands.shape or []))))
+    return lo, sh
+
+
+class ExclusionMask:
+    """The exclusion of acquisition.py:137-139 -- a candidate equal in every coordinate to an
+    evaluated point is never selected -- as a device bit mask over one candidate shard
+    ([offset, offset + count) of `cands`), kept across iterations (bo_excl_mask_update).
+
+    The loop's evaluated set only grows (x_vector[:n], the new batch appended each iteration),
+    so `update(points)` adds the rows it has not seen yet: one thread per new point on a grid,
+    one pass over the shard otherwise.  A shorter or changed prefix rebuilds the mask.  The
+    masked selections (bo_select_topq_masked, bo_hvi_select_topq_masked) then drop an excluded
+    element as they load it: no per-call hash set and no probes."""
+
+    def __init__(self, cands, offset=0, count=None, device=None):
+        self.cands = cands
+        self.offset = int(offset)
+        self.count = int(cands.n - offset if count is None else count)
+        self.dev = require_device(device)
+        lib = _lib.load()
+        self.bits = torch.zeros(lib.bo_excl_mask_bytes(self.count) // 4, dtype=torch.int32, device=self.dev)
+        self.n_seen = 0
+        self._seen = None              # host copy of the rows already in the mask
+
+    @property
+    def ptr(self):
+        return self.bits.data_ptr()
+
+    def update(self, evaluated_points):
+        ev = np.ascontiguousarray(np.asarray(evaluated_points.cpu().numpy() if isinstance(evaluated_points, torch.Tensor)
+                                             else evaluated_points, dtype=np.float64).reshape(-1, self.cands.dim))
+        n = ev.shape[0]
+        clear = n < self.n_seen or (self.n_seen > 0 and not np.array_equal(ev[: self.n_seen], self._seen))
+        first = 0 if clear else self.n_seen
+        if first == n and not clear:
+            return self
+        lib = _lib.load()
+        ex = torch.as_tensor(ev, device=self.dev)
+        ws = Workspace.get(lib.bo_excl_mask_workspace_size(n - first), self.dev)
+        lo, sh = _grid_args(self.cands)
+        carg = self.cands.cand_arg
+        if self.cands.kind in ("i64", "f64"):
+            carg = self.cands.tensor[self.offset:].data_ptr()
+        _lib.check(lib.bo_excl_mask_update(self.ptr, self.count, self.cands.kind_code, carg, lo, sh,
+                                           self.cands.dim, self.offset, ex.data_ptr() if n else None, first, n,
+                                           1 if clear else 0, ws.data_ptr(), ws.numel(),
+                                           stream_handle(self.dev)), "bo_excl_mask_update")
+        self._keep = ex                # the points stay alive until the stream has used them
+        self.n_seen = n
+        self._seen = ev.copy()
+        return self
+
+    def excluded(self):
+        """Host bool array [count]: the candidates the mask excludes."""
+        w = self.bits.cpu().numpy().view(np.uint32)
+        return np.unpackbits(w.view(np.uint8), bitorder="little")[: self.count].astype(bool)
+
+
+def select_indices(acquisition_values, cands, evaluated_points, batch_size, dev=None, mask=None):
     """Global candidate indices of select_next_batch's choice (device top-q with exclusion).
 
     Order: NaN first, then descending value, ties by ascending index (the reference's
     argsort tie order is unspecified).  Batches above BO_MAX_TOPQ are taken in rounds,
-    each round excluding the points already chosen.
+    each round excluding the points already chosen.  `mask` (an ExclusionMask of the whole set,
+    already updated with evaluated_points) replaces the per-call exclusion when the batch fits
+    one call.
     """
     dev = dev or _dev_of(acquisition_values, evaluated_points)
     acq = _Arg(acquisition_values, dev)
+    lib = _lib.load()
+    if mask is not None and batch_size <= _lib.MAX_TOPQ:
+        tv = torch.empty(batch_size, dtype=F64, device=dev)
+        ti = torch.empty(batch_size, dtype=torch.int64, device=dev)
+        ws = Workspace.get(lib.bo_select_topq_workspace_size(cands.n, batch_size), dev)
+        _lib.check(lib.bo_select_topq_masked(acq.ptr, cands.n, 0, mask.ptr, batch_size, tv.data_ptr(),
+                                             ti.data_ptr(), ws.data_ptr(), ws.numel(), stream_handle(dev)),
+                   "bo_select_topq_masked")
+        got = ti.cpu().numpy()
+        return got[got >= 0].astype(np.int64)
     ev = np.asarray(evaluated_points.cpu().numpy() if isinstance(evaluated_points, torch.Tensor)
                     else evaluated_points, dtype=np.float64).reshape(-1, cands.dim)
-    lib = _lib.load()
     chosen = []
     while len(chosen) < batch_size:
         q = min(_lib.MAX_TOPQ, batch_size - len(chosen))
@@ -71,8 +143,7 @@ def select_indices(acquisition_values, cands, evaluated_points, batch_size, dev=
         ex = torch.as_tensor(np.ascontiguousarray(excl), device=dev)
         tv = torch.empty(q, dtype=F64, device=dev)
         ti = torch.empty(q, dtype=torch.int64, device=dev)
-        lo = (C_i64 * 8)(*(list(cands.lo or []) + [0] * (8 - len(cands.lo or []))))
-        sh = (C_i64 * 8)(*(list(cands.shape or []) + [1] * (8 - len(cands.shape or []))))
+        lo, sh = _grid_args(cands)
         nbytes = lib.bo_select_topq_workspace_size(cands.n, q)
         ws = Workspace.get(nbytes, dev)
         _lib.check(lib.bo_select_topq(acq.ptr, cands.n, cands.kind_code, cands.cand_arg, lo, sh, cands.dim, 0, ex.data_ptr() if ex.numel() else None,
@@ -147,13 +218,16 @@ def hypervolume_improvement_exact(ucb, front, reference_point, prior_mean, prior
 
 
 def hvi_select_indices(acquisition_values, ucb, y_vector, n_evaluations, reference_point, prior_mean,
-                       prior_variance, cands, evaluated_points, batch_size, offset=0, return_record=False):
+                       prior_variance, cands, evaluated_points, batch_size, offset=0, return_record=False,
+                       mask=None):
     """The exact-HVI acquisition AND its batch selection in one device pass (bo_hvi_select_topq,
     batch_size <= BO_MAX_TOPQ): acquisition_values (device, [count]) receives the HVI of the UCB
     vector of every candidate of the shard [offset, offset + count) over the Pareto front of
     y_vector[:n_evaluations]; returns the global indices of the shard's best batch_size candidates
     not equal to an evaluated point (select_next_batch's order) -- or, `return_record`, the device
-    record block [2 batch_size] (values, bit-cast int64 indices) for the multi-rank exchange."""
+    record block [2 batch_size] (values, bit-cast int64 indices) for the multi-rank exchange.
+    `mask`: this shard's ExclusionMask (updated here with evaluated_points; only the new rows
+    are added) -- the selection then runs bo_hvi_select_topq_masked."""
     from .pareto import is_pareto_efficient
     if batch_size > _lib.MAX_TOPQ:
         raise ValueError(f"hvi_select_indices handles batch_size <= {_lib.MAX_TOPQ}")
@@ -166,25 +240,34 @@ def hvi_select_indices(acquisition_values, ucb, y_vector, n_evaluations, referen
     acq = _Arg(acquisition_values, dev, write=True)
     n_obj, n = u.t.shape
     boxes = torch.as_tensor(hypervolume_boxes(front, reference_point), device=dev)
-    ev = np.asarray(evaluated_points.cpu().numpy() if isinstance(evaluated_points, torch.Tensor)
-                    else evaluated_points, dtype=np.float64).reshape(-1, cands.dim)
-    ex = torch.as_tensor(np.ascontiguousarray(ev), device=dev)
     rec = torch.empty(2 * batch_size, dtype=F64, device=dev)
     lib = _lib.load()
     ws = Workspace.get(lib.bo_select_topq_workspace_size(n, batch_size), dev)
-    lo = (C_i64 * 8)(*(list(cands.lo or []) + [0] * (8 - len(cands.lo or []))))
-    sh = (C_i64 * 8)(*(list(cands.shape or []) + [1] * (8 - len(cands.shape or []))))
     shift = _host_vec(prior_mean, n_obj)
     scale = _host_vec(np.sqrt(np.asarray(prior_variance, dtype=np.float64)), n_obj)
-    carg = cands.cand_arg
-    if cands.kind in ("i64", "f64"):            # explicit candidates: the shard's rows
-        carg = cands.tensor[offset:].data_ptr()
-    _lib.check(lib.bo_hvi_select_topq(acq.ptr, u.ptr, u.t.stride(0), n, n_obj, shift, scale,
-                                      boxes.data_ptr() if boxes.numel() else None, boxes.shape[0],
-                                      cands.kind_code, carg, lo, sh, cands.dim, offset,
-                                      ex.data_ptr() if ex.numel() else None, ex.shape[0], batch_size,
-                                      rec.data_ptr(), rec.data_ptr() + 8 * batch_size, ws.data_ptr(),
-                                      ws.numel(), stream_handle(dev)), "bo_hvi_select_topq")
+    if mask is not None:
+        if mask.offset != offset or mask.count != n:
+            raise ValueError("hvi_select_indices: the mask covers another shard")
+        mask.update(evaluated_points)
+        _lib.check(lib.bo_hvi_select_topq_masked(acq.ptr, u.ptr, u.t.stride(0), n, n_obj, shift, scale,
+                                                 boxes.data_ptr() if boxes.numel() else None, boxes.shape[0],
+                                                 offset, mask.ptr, batch_size, rec.data_ptr(),
+                                                 rec.data_ptr() + 8 * batch_size, ws.data_ptr(), ws.numel(),
+                                                 stream_handle(dev)), "bo_hvi_select_topq_masked")
+    else:
+        ev = np.asarray(evaluated_points.cpu().numpy() if isinstance(evaluated_points, torch.Tensor)
+                        else evaluated_points, dtype=np.float64).reshape(-1, cands.dim)
+        ex = torch.as_tensor(np.ascontiguousarray(ev), device=dev)
+        lo, sh = _grid_args(cands)
+        carg = cands.cand_arg
+        if cands.kind in ("i64", "f64"):            # explicit candidates: the shard's rows
+            carg = cands.tensor[offset:].data_ptr()
+        _lib.check(lib.bo_hvi_select_topq(acq.ptr, u.ptr, u.t.stride(0), n, n_obj, shift, scale,
+                                          boxes.data_ptr() if boxes.numel() else None, boxes.shape[0],
+                                          cands.kind_code, carg, lo, sh, cands.dim, offset,
+                                          ex.data_ptr() if ex.numel() else None, ex.shape[0], batch_size,
+                                          rec.data_ptr(), rec.data_ptr() + 8 * batch_size, ws.data_ptr(),
+                                          ws.numel(), stream_handle(dev)), "bo_hvi_select_topq")
     acq.finish()
     if return_record:
         return rec

@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from .acquisition import hvi_select_indices, select_indices, update_hypervolume_improvement_exact
+from .acquisition import ExclusionMask, hvi_select_indices, select_indices, update_hypervolume_improvement_exact
 from .config import (DEFAULT_BATCH_SIZE, DEFAULT_BETA, DEFAULT_INITIAL_SAMPLES,
                      DEFAULT_LENGTH_SCALE, DEFAULT_PRIOR_MEAN, DEFAULT_PRIOR_VARIANCE,
                      resolve_float_type)
@@ -133,6 +133,7 @@ class DeviceBackend:
         self.bufs = buffers
         self._lu_hint = None           # per objective: the previous invert_k took the LU path
         self.inverse_paths = []
+        self._excl_mask = None         # the shard's ExclusionMask (exact-HVI selection)
 
     def fit(self, x_vector, y_vector, n, prior_mean, prior_variance, length_scales):
         """Returns (Powell's OptimizeResult, fitted device state, time after the Powell fit)."""
@@ -147,13 +148,53 @@ class DeviceBackend:
         # an objective whose Cholesky failed last iteration (Powell-fitted length scales drive
         # cond(K + 1e-6 I) past 1e16) fails again: when all did, go straight to the
         # blocked LU -- gesv's algorithm, the reference's own -- without the doomed attempt
-        paths = []
-        kinv = K.invert_k(n, self.bufs.kernel_matrices, float_type=self.float_type, lu_hint=self._lu_hint,
-                          paths=paths)
-        self._lu_hint = [p != 0 for p in paths]
-        self.inverse_paths = paths
+        from .distributed import collectives_on
+        if self.world > 1 and collectives_on(self.group):
+            kinv = self._invert_split(n)
+        else:
+            paths = []
+            kinv = K.invert_k(n, self.bufs.kernel_matrices, float_type=self.float_type, lu_hint=self._lu_hint,
+                              paths=paths)
+            self._lu_hint = [p != 0 for p in paths]
+            self.inverse_paths = paths
         torch.cuda.synchronize(self.dev)
         return optimized, (xd, yd, kinv), t1
+
+    def _invert_split(self, n):
+        """invert_k with the objectives split over the ranks (objective o on rank o mod P), each
+        K^-1 then broadcast from its rank (one broadcast per objective: n^2 doubles, 2 MiB at C3).
+        Each objective's inverse is the same per-objective device computation as in the batched
+        single-rank call, so every rank holds the single-rank K^-1 bit for bit."""
+        import torch.distributed as dist
+        km = self.bufs.kernel_matrices
+        n_obj = km.shape[0]
+        mine = [o for o in range(n_obj) if o % self.world == self.rank]
+        kinv = torch.empty((n_obj, n, n), dtype=F64, device=self.dev)
+        hint = self._lu_hint or [False] * n_obj
+        paths = [0] * n_obj
+        if mine:
+            sub = km[mine] if len(mine) > 1 else km[mine[0]:mine[0] + 1]
+            p = []
+            got = K.invert_k(n, sub.contiguous(), float_type=self.float_type, lu_hint=[hint[o] for o in mine],
+                             paths=p)
+            for i, o in enumerate(mine):
+                kinv[o] = got[i]
+                paths[o] = p[i]
+        nccl = dist.get_backend(self.group) == "nccl"
+        for o in range(n_obj):
+            src = o % self.world                    # a group rank; broadcast takes the global one
+            if self.group is not None:
+                src = dist.get_global_rank(self.group, src)
+            if nccl:
+                dist.broadcast(kinv[o], src=src, group=self.group)
+            else:                                   # gloo: the collective on a host copy
+                h = kinv[o].cpu()
+                dist.broadcast(h, src=src, group=self.group)
+                kinv[o].copy_(h)
+        # the path hints follow the objectives this rank inverts (o mod P is fixed)
+        self._lu_hint = [paths[o] != 0 if o in mine else hint[o] for o in range(n_obj)]
+        self.inverse_paths = paths
+        return kinv
 
     def _outputs(self):
         b = self.bufs
@@ -183,10 +224,14 @@ class DeviceBackend:
         if acquisition == "hvi" and batch_size <= _lib.MAX_TOPQ:
             # the exact HVI and its top-q with exclusion in one device pass over this shard, then
             # the fused path's exchange
+            # the shard's exclusion mask persists across iterations: only the new batch's rows
+            # are added to it (ExclusionMask)
+            if self._excl_mask is None:
+                self._excl_mask = ExclusionMask(self.cands, self.offset, self.count, self.dev)
             rec = hvi_select_indices(self.bufs.acquisition_values, self.bufs.ucb, y_evaluated,
                                      len(y_evaluated), reference_point, prior_mean, prior_variance,
                                      self.cands, evaluated, batch_size, offset=self.offset,
-                                     return_record=True)
+                                     return_record=True, mask=self._excl_mask)
             from .distributed import collectives_on, exchange_topq_rec
             if not collectives_on(self.group):
                 idx = rec[batch_size:].view(torch.int64).cpu().numpy()

@@ -117,11 +117,20 @@ struct SelArgs {
   long long partial_cap;    // entries of `partial` (the debug build checks every write)
   int idx32;                // grid: every global index below 2^31 (32-bit decode)
   SobolArgs sob;            // kind BO_CAND_SOBOL
+  // candidate exclusion mask (bo_excl_mask_update): bit j of word j / 32 set = local candidate j
+  // equals an evaluated point.  When given, an excluded element is dropped as it is loaded (key
+  // 0, as an out-of-range one) and n_excl is 0: no hash, no probes.
+  const unsigned int* xbits;
 };
 
+__device__ __forceinline__ bool xbit(const unsigned int* xb, long long j) {
+  return xb && ((xb[j >> 5] >> (j & 31)) & 1u);
+}
+
 __global__ void excl_hash_kernel(unsigned long long* __restrict__ keys, int* __restrict__ idx,
-                                 unsigned int mask, const double* __restrict__ excl, int n_excl, int dim) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+                                 unsigned int mask, const double* __restrict__ excl, int first,
+                                 int n_excl, int dim) {
+  const int e = first + blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_excl) return;
   const unsigned long long key = bo_point_key(excl + (long long)e * dim, dim);
   if (key != 0ull) bo_hash_insert(keys, idx, mask, key, e);
@@ -178,6 +187,45 @@ __device__ __forceinline__ double cand_coord(const SelArgs& a, long long j, int 
   long long gi = a.cand_offset + j;
   for (int t = a.dim - 1; t > k; --t) gi /= a.grid_shape[t];
   return (double)(a.grid_lo[k] + gi % a.grid_shape[k]);
+}
+
+// ---------------------------------------------------------------------------------------
+// The candidate exclusion mask (bo_excl_mask_update): the set acquisition.py:137-139 tests
+// per candidate -- "equal in every coordinate to an evaluated point" -- as one bit per local
+// candidate index, built once per iteration (or extended by the q new points), so that the
+// selection drops an excluded element as it loads it.
+// Grid candidates (every coordinate below 2^53): point e maps to at most one grid index, found
+// arithmetically -- each coordinate must be an integer lo_k + t_k, 0 <= t_k < shape_k.
+__global__ void excl_mask_grid_kernel(unsigned int* __restrict__ bits, SelArgs a, int first) {
+  const int e = first + blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n_excl) return;
+  const double* p = a.excl + (long long)e * a.dim;
+  long long gi = 0;
+  for (int k = 0; k < a.dim; ++k) {
+    const double x = p[k];
+    const double lo = (double)a.grid_lo[k];
+    // NaN or outside [lo, lo + shape) or not an integer: no candidate equals it
+    if (!(x >= lo && x < lo + (double)a.grid_shape[k]) || x != __builtin_floor(x)) return;
+    gi = gi * a.grid_shape[k] + ((long long)x - a.grid_lo[k]);
+  }
+  const long long j = gi - a.cand_offset;
+  if (j < 0 || j >= a.n_cand) return;
+  atomicOr(bits + (j >> 5), 1u << (j & 31));
+}
+
+// Any other candidate kind: every candidate probes the hash set of the points (global memory);
+// a wave's 64 consecutive candidates set their bits with at most two atomics.
+__global__ void excl_mask_scan_kernel(unsigned int* __restrict__ bits, SelArgs a,
+                                      const unsigned long long* __restrict__ hk,
+                                      const int* __restrict__ hi, unsigned int hm) {
+  const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim 256
+  const bool hit = j < a.n_cand && cand_excluded(a, j, hk, hi, hm);
+  const unsigned long long b = __ballot(hit);
+  if ((threadIdx.x & 63) == 0 && b) {
+    const long long w = j >> 5;                  // j is a multiple of 64 in lane 0
+    if ((unsigned int)b) atomicOr(bits + w, (unsigned int)b);
+    if ((unsigned int)(b >> 32)) atomicOr(bits + w + 1, (unsigned int)(b >> 32));
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -483,6 +531,81 @@ __device__ __forceinline__ void block_span_select(LaneRun<U>& r, double& lv, lon
   wave_extract<U>(r, bk, bi, lv, li, q, rbuf, excluded, wk, wi);
 }
 
+// ---------------------------------------------------------------------------------------
+// The lean form, when no element needs an exclusion probe (an exclusion mask dropped the
+// evaluated points at load, or there are none): the top-q of a wave is q rounds of the wave
+// arg-best over the lanes' sorted runs (the owner lane of each winner moves to its next entry),
+// produced in selection order -- no bound, no rank insertion -- and the workgroup's top-q is
+// q more rounds in wave 0 over the NW x q wave results, one per lane.
+// ---------------------------------------------------------------------------------------
+// acc := the best U entries (sorted) of acc and nx (both sorted): a bitonic merge
+template <int U>
+__device__ __forceinline__ void lane_keep_best(LaneRun<U>& acc, const LaneRun<U>& nx) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool t = kbefore(nx.k[U - 1 - u], nx.i[U - 1 - u], acc.k[u], acc.i[u]);
+    acc.k[u] = t ? nx.k[U - 1 - u] : acc.k[u];
+    acc.i[u] = t ? nx.i[U - 1 - u] : acc.i[u];
+  }
+  auto cx = [&](int x, int y) {
+    const bool sw = kbefore(acc.k[y], acc.i[y], acc.k[x], acc.i[x]);
+    const unsigned long long tk = acc.k[x];
+    const long long ti = acc.i[x];
+    acc.k[x] = sw ? acc.k[y] : acc.k[x];
+    acc.i[x] = sw ? acc.i[y] : acc.i[x];
+    acc.k[y] = sw ? tk : acc.k[y];
+    acc.i[y] = sw ? ti : acc.i[y];
+  };
+  if constexpr (U == 2) cx(0, 1);
+  if constexpr (U == 4) { cx(0, 2); cx(1, 3); cx(0, 1); cx(2, 3); }
+}
+
+// q rounds of the wave arg-best over the lanes' runs (r.h = 0 on entry): round t's winner is
+// the wave's t-th best.  Lane t of the wave receives it in (tk, ti) (key 0 / -1: none left).
+template <int U>
+__device__ __forceinline__ void wave_topq_rounds(LaneRun<U>& r, int q, unsigned long long& tk, long long& ti) {
+  const int lane = threadIdx.x & 63;
+  tk = 0ull;
+  ti = -1;
+  for (int t = 0; t < q; ++t) {
+    unsigned long long hk;
+    long long hi;
+    r.head(hk, hi);
+    unsigned long long wk;
+    long long wi;
+    wave_argbest(hk, hi, wk, wi);
+    if (wk == 0ull) break;                       // wave-uniform: nothing left
+    if (hi == wi) ++r.h;                         // the owner moves on (valid indices are distinct)
+    if (lane == t) { tk = wk; ti = wi; }
+  }
+}
+
+// The workgroup's top-q (q <= 16) of its NW waves' runs: the waves' rounds, their lists through
+// LDS (wl: NW * q entries), q rounds in wave 0.  Lane t < q of wave 0 returns entry t in (ov, oi)
+// (-inf / -1 when fewer exist); the other waves return at once.  Every thread calls it.
+template <int U>
+__device__ __forceinline__ bool block_topq_rounds(LaneRun<U>& r, int q, int nw, TopEntry* wl, double& ov,
+                                                  long long& oi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long tk;
+  long long ti;
+  r.h = 0;
+  wave_topq_rounds<U>(r, q, tk, ti);
+  if (lane < q) { wl[wave * q + lane].v = tk ? bo_key_value(tk) : -__builtin_inf(); wl[wave * q + lane].i = ti; }
+  __syncthreads();
+  if (wave != 0) return false;
+  LaneRun<1> m;
+  const bool mine = lane < nw * q;
+  const TopEntry e = mine ? wl[lane] : TopEntry{-__builtin_inf(), -1};
+  m.k[0] = e.i >= 0 ? bo_order_key(e.v, 0) : 0ull;
+  m.i[0] = e.i;
+  m.h = 0;
+  wave_topq_rounds<1>(m, q, tk, ti);
+  ov = tk ? bo_key_value(tk) : -__builtin_inf();
+  oi = ti;
+  return true;
+}
+
 // Diagnostic build (BO_BUILD_VARIANT=DEF_SEL_TIMING): phase stamps of workgroups 0 and the last
 // (wave 0, real-time clock, 10 ns ticks) printed at the end of select_small_kernel.
 #ifdef BO_SEL_TIMING
@@ -512,15 +635,16 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
 #endif
   SEL_STAMP(0);
   LaneRun<U> run;
-  auto load_span = [&](long long s0) {
+  auto load_span = [&](long long s0, LaneRun<U>& dst) {
     if constexpr (M == 0) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long long j = s0 + wave * wspan + 64 * u + lane;
         const bool in = j < a.n_cand;
         const double v = in ? __builtin_nontemporal_load(a.acq + j) : 0.0;
-        run.i[u] = in ? a.cand_offset + j : -1;
-        run.k[u] = in ? bo_order_key(v, 0) : 0ull;
+        const bool ok = in && !xbit(a.xbits, j);
+        dst.i[u] = ok ? a.cand_offset + j : -1;
+        dst.k[u] = ok ? bo_order_key(v, 0) : 0ull;
       }
     } else {
       // the U elements' UCB loads first, then the boxes outer: one (wave-uniform) load of a box
@@ -562,13 +686,44 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
         const bool in = j < a.n_cand;
         const double v = nan[u] ? __builtin_nan("") : hv[u];
         if (in) h.acq_out[j] = v;
-        run.i[u] = in ? a.cand_offset + j : -1;
-        run.k[u] = in ? bo_order_key(v, 0) : 0ull;
+        const bool ok = in && !xbit(a.xbits, j);
+        dst.i[u] = ok ? a.cand_offset + j : -1;
+        dst.k[u] = ok ? bo_order_key(v, 0) : 0ull;
       }
     }
   };
   // the first span's loads go out before the hash build (they need no table)
-  if (b_first < a.n_cand) load_span(b_first);
+  if (b_first < a.n_cand) load_span(b_first, run);
+  if (a.n_excl == 0) {
+    // lean form: nothing to probe (the exclusion mask dropped the evaluated points at load, or
+    // there are none); a lane keeps the best U of all its spans, then the rounds
+    if (b_first >= a.n_cand) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) { run.k[u] = 0ull; run.i[u] = -1; }
+    }
+    run.sort();
+    for (long long s0 = b_first + b_stride; s0 < a.n_cand; s0 += b_stride) {   // workgroup-uniform
+      LaneRun<U> nx;
+      load_span(s0, nx);
+      nx.sort();
+      lane_keep_best<U>(run, nx);
+    }
+#ifdef BO_SEL_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    SEL_STAMP(1);
+    double ov;
+    long long oi;
+    const bool w0 = block_topq_rounds<U>(run, q, 16, wl, ov, oi);
+    if (w0 && lane < q) a.partial[(size_t)blockIdx.x * q + lane] = TopEntry{ov, oi};
+#ifdef BO_SEL_TIMING
+    SEL_STAMP(2);
+    if ((blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && threadIdx.x == 0)
+      printf("lean sel block %d: loads %lld rounds %lld ticks (x10 ns)\n", (int)blockIdx.x, _t[1] - _t[0],
+             _t[2] - _t[1]);
+#endif
+    return;
+  }
   if (a.lds_slots > 0) {
     int* lidx = (int*)(lkeys + a.lds_slots);
     for (int t = tid; t < a.lds_slots; t += blockDim.x) lkeys[t] = 0ull;
@@ -588,7 +743,7 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
   double lv = -__builtin_inf();
   long long li = -1;
   for (long long s0 = b_first; s0 < a.n_cand; s0 += b_stride) {     // workgroup-uniform
-    if (s0 != b_first) load_span(s0);
+    if (s0 != b_first) load_span(s0, run);
 #ifdef BO_SEL_TIMING
     __builtin_amdgcn_s_waitcnt(0);
 #endif
@@ -604,6 +759,28 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
     printf("sel block %d wave %d: hash %lld loads %lld span %lld merge %lld ticks (x10 ns)\n", (int)blockIdx.x,
            (int)(threadIdx.x >> 6), _t[1] - _t[0], _t[2] - _t[1], _t[3] - _t[2], _t[4] - _t[3]);
 #endif
+}
+
+// Final merge of n_lists <= 1024 sorted top-q lists ([n_lists][q], q <= 4): one workgroup, a lane
+// per list, the lean rounds (block_topq_rounds) -- the lists hold no evaluated point.
+__global__ __launch_bounds__(1024) void select_rounds_merge_kernel(const TopEntry* __restrict__ L, int n_lists,
+                                                                   int q, double* __restrict__ out_v,
+                                                                   long long* __restrict__ out_i) {
+  __shared__ TopEntry wl[16 * 4];
+  const int l = threadIdx.x, lane = l & 63;
+  LaneRun<4> run;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const TopEntry e = (l < n_lists && u < q) ? L[(size_t)l * q + u] : TopEntry{-__builtin_inf(), -1};
+    run.i[u] = e.i;
+    run.k[u] = e.i >= 0 ? bo_order_key(e.v, 0) : 0ull;
+  }
+  double ov;
+  long long oi;
+  if (block_topq_rounds<4>(run, q, (int)(blockDim.x >> 6), wl, ov, oi) && lane < q) {
+    out_v[lane] = ov;
+    out_i[lane] = oi;
+  }
 }
 
 // Final merge of n_lists sorted top-q lists ([n_lists][q], q <= U <= 16): one workgroup of 4
@@ -683,11 +860,13 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
   // wave-uniform trip count: every lane stays in the loop for the ballots and broadcasts
   for (long long b0 = b_first; b0 < a.n_cand; b0 += U * stride) {
     double val[U];
+    bool live[U];                     // in range and not masked out (xbits)
     bool any = false;
 #pragma unroll
     for (int u = 0; u < U; ++u) {     // all U loads in flight before any element is looked at
       const long long j = b0 + u * stride + lane;
       const bool in = j < a.n_cand;
+      live[u] = in && !xbit(a.xbits, j);
       if constexpr (M == 0) {
         val[u] = b0 == b_first ? pre[u] : (in ? a.acq[j] : 0.0);
       } else {
@@ -712,7 +891,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
         val[u] = nan ? __builtin_nan("") : hv;
         if (in) h.acq_out[j] = val[u];
       }
-      any = any || (in && !(val[u] < tv));
+      any = any || (live[u] && !(val[u] < tv));
     }
     if (__ballot(any) == 0ull) continue;
     // ---- event: the elements beating T (exact order) are pending
@@ -720,7 +899,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long j = b0 + u * stride + lane;
-      pend[u] = j < a.n_cand && bo_better(val[u], a.cand_offset + j, tv, ti);
+      pend[u] = live[u] && bo_better(val[u], a.cand_offset + j, tv, ti);
     }
     for (;;) {
       int cnt = 0;
@@ -977,7 +1156,18 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
                 const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
                 int64_t cand_offset, const double* excl, int64_t n_excl, int32_t topq,
                 double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes, hipStream_t s,
-                const HviIn* h, int m) {
+                const HviIn* h, int m, const unsigned int* xbits = nullptr) {
+  static const int64_t kOne[BO_MAX_DIM] = {1, 1, 1, 1, 1, 1, 1, 1};
+  static const int64_t kZero[BO_MAX_DIM] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (xbits) {                            // the mask replaces the points: no candidate decode
+    kind = BO_CAND_GRID;
+    cand = nullptr;
+    grid_lo = kZero;
+    grid_shape = kOne;
+    dim = 1;
+    excl = nullptr;
+    n_excl = 0;
+  }
   if ((!acq && m == 0) || topq < 1 || topq > BO_MAX_TOPQ || dim < 1 || dim > BO_MAX_DIM ||
       n_cand < 0 || !top_val || !top_idx || (n_excl > 0 && !excl) || kind < 0 || kind > BO_CAND_SOBOL)
     return BO_ERR_ARG;
@@ -986,6 +1176,7 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   if (!ws || ws_bytes < bo_select_topq_workspace_size(n_cand, topq)) return BO_ERR_WORKSPACE;
   SelArgs a;
   memset(&a, 0, sizeof(a));
+  a.xbits = xbits;
   a.acq = acq;
   a.n_cand = n_cand;
   a.cand_offset = cand_offset;
@@ -1026,7 +1217,7 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
       int* idx = (int*)(keys + slots);
       BO_CHECK_HIP(hipMemsetAsync(keys, 0, (size_t)slots * 8, s));
       hipLaunchKernelGGL(excl_hash_kernel, dim3((unsigned)((n_excl + 255) / 256)), dim3(256), 0, s,
-                         keys, idx, slots - 1, excl, (int)n_excl, dim);
+                         keys, idx, slots - 1, excl, 0, (int)n_excl, dim);
       BO_CHECK_HIP(hipGetLastError());
       a.hkeys = keys;
       a.hidx = idx;
@@ -1053,9 +1244,15 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
       default: return BO_ERR_UNSUPPORTED;
     }
     if (st != BO_OK) return st;
-    static_assert(kSmallQ <= 4, "select_merge_kernel<4> holds q <= 4 entries per list");
-    hipLaunchKernelGGL(select_merge_kernel<4>, dim3(1), dim3(256), 0, s, (const TopEntry*)ws, blocks,
-                       topq, top_val, (long long*)top_idx);
+    static_assert(kSmallQ <= 4, "the merge kernels hold q <= 4 entries per list");
+    if (blocks <= 1024) {          // a lane per list (blocks <= 1024 always: max_blocks above)
+      const unsigned threads = (unsigned)((blocks + 63) / 64 * 64);
+      hipLaunchKernelGGL(select_rounds_merge_kernel, dim3(1), dim3(threads), 0, s, (const TopEntry*)ws,
+                         (int)blocks, topq, top_val, (long long*)top_idx);
+    } else {
+      hipLaunchKernelGGL(select_merge_kernel<4>, dim3(1), dim3(256), 0, s, (const TopEntry*)ws, blocks,
+                         topq, top_val, (long long*)top_idx);
+    }
     BO_CHECK_HIP(hipGetLastError());
     return BO_OK;
   }
@@ -1113,6 +1310,110 @@ int bo_hvi_select_topq(double* acq, const double* ucb, int64_t ld, int64_t n_can
   h.acq_out = acq;
   return select_impl(acq, n_cand, kind, cand, grid_lo, grid_shape, dim, cand_offset, excl, n_excl,
                      topq, top_val, top_idx, ws, ws_bytes, s, &h, n_obj);
+}
+
+size_t bo_excl_mask_bytes(int64_t n_cand) {
+  const size_t words = ((size_t)(n_cand > 0 ? n_cand : 0) + 31) / 32 + 2;
+  return (words * 4 + 255) / 256 * 256;
+}
+
+size_t bo_excl_mask_workspace_size(int64_t n_excl) {
+  return (size_t)bo_hash_slots(n_excl > 0 ? n_excl : 0) * 12 + 256;
+}
+
+int bo_excl_mask_update(uint32_t* mask, int64_t n_cand, int32_t kind, const void* cand,
+                        const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
+                        int64_t cand_offset, const double* excl, int64_t first_excl, int64_t n_excl,
+                        int32_t clear, void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!mask || n_cand < 0 || dim < 1 || dim > BO_MAX_DIM || first_excl < 0 || n_excl < first_excl ||
+      n_excl > (1LL << 30) || (n_excl > first_excl && !excl) || kind < 0 || kind > BO_CAND_SOBOL)
+    return BO_ERR_ARG;
+  if (kind != BO_CAND_GRID && !cand) return BO_ERR_ARG;
+  if (kind == BO_CAND_GRID && (!grid_lo || !grid_shape)) return BO_ERR_ARG;
+  if (clear) BO_CHECK_HIP(hipMemsetAsync(mask, 0, bo_excl_mask_bytes(n_cand), s));
+  if (n_excl == first_excl || n_cand == 0) return BO_OK;
+  SelArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n_cand = n_cand;
+  a.cand_offset = cand_offset;
+  a.kind = kind;
+  a.dim = dim;
+  a.n_excl = (int)n_excl;
+  a.cand = cand;
+  a.excl = excl;
+  for (int k = 0; k < BO_MAX_DIM; ++k) a.grid_shape[k] = 1;
+  bool arith = kind == BO_CAND_GRID;
+  if (kind == BO_CAND_SOBOL) {
+    const int st = bo_sobol_fill(&a.sob, dim, (const bo_sobol_desc*)cand);
+    if (st != BO_OK) return st;
+    a.cand = nullptr;
+  }
+  if (kind == BO_CAND_GRID) {
+    unsigned long long total = 1;
+    for (int k = 0; k < dim; ++k) {
+      if (grid_shape[k] <= 0) return BO_ERR_ARG;
+      a.grid_lo[k] = grid_lo[k];
+      a.grid_shape[k] = grid_shape[k];
+      const long long lim = 1LL << 53;          // every grid coordinate exact in f64
+      if (grid_lo[k] <= -lim || grid_lo[k] >= lim || grid_shape[k] >= lim - grid_lo[k]) arith = false;
+      total = total * (unsigned long long)grid_shape[k];
+      if (total >= (1ull << 62)) arith = false;
+    }
+    a.idx32 = cand_offset >= 0 && cand_offset + n_cand < (1LL << 31) ? 1 : 0;
+    for (int k = 0; k < dim; ++k)
+      if (grid_shape[k] >= (1LL << 31)) a.idx32 = 0;
+  }
+  const int first = (int)first_excl, cnt = (int)(n_excl - first_excl);
+  if (arith) {
+    hipLaunchKernelGGL(excl_mask_grid_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s,
+                       (unsigned int*)mask, a, first);
+    BO_CHECK_HIP(hipGetLastError());
+    return BO_OK;
+  }
+  // hash set of the new points (rows first .. n_excl) in the workspace, then the candidate scan
+  const unsigned int slots = bo_hash_slots(cnt);
+  if (!ws || ws_bytes < bo_excl_mask_workspace_size(cnt)) return BO_ERR_WORKSPACE;
+  unsigned long long* keys = (unsigned long long*)ws;
+  int* idx = (int*)(keys + slots);
+  BO_CHECK_HIP(hipMemsetAsync(keys, 0, (size_t)slots * 8, s));
+  hipLaunchKernelGGL(excl_hash_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, keys, idx,
+                     slots - 1, excl, first, (int)n_excl, dim);
+  BO_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(excl_mask_scan_kernel, dim3((unsigned)((n_cand + 255) / 256)), dim3(256), 0, s,
+                     (unsigned int*)mask, a, (const unsigned long long*)keys, (const int*)idx, slots - 1);
+  BO_CHECK_HIP(hipGetLastError());
+  return BO_OK;
+}
+
+int bo_select_topq_masked(const double* acq, int64_t n_cand, int64_t cand_offset, const uint32_t* mask,
+                          int32_t topq, double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes,
+                          void* stream) {
+  if (!mask) return BO_ERR_ARG;
+  return select_impl(acq, n_cand, BO_CAND_GRID, nullptr, nullptr, nullptr, 1, cand_offset, nullptr, 0,
+                     topq, top_val, top_idx, ws, ws_bytes, (hipStream_t)stream, nullptr, 0,
+                     (const unsigned int*)mask);
+}
+
+int bo_hvi_select_topq_masked(double* acq, const double* ucb, int64_t ld, int64_t n_cand, int32_t n_obj,
+                              const double* shift, const double* scale, const double* boxes,
+                              int64_t n_boxes, int64_t cand_offset, const uint32_t* mask, int32_t topq,
+                              double* top_val, int64_t* top_idx, void* ws, size_t ws_bytes,
+                              void* stream) {
+  if (!acq || !ucb || !shift || !scale || !mask || n_obj < 1 || n_obj > 4 || ld < n_cand ||
+      n_boxes < 0 || (n_boxes > 0 && !boxes))
+    return BO_ERR_ARG;
+  HviIn h;
+  memset(&h, 0, sizeof(h));
+  h.ucb = ucb;
+  h.ld = ld;
+  h.boxes = boxes;
+  h.n_boxes = n_boxes;
+  for (int k = 0; k < n_obj; ++k) { h.shift[k] = shift[k]; h.scale[k] = scale[k]; }
+  h.acq_out = acq;
+  return select_impl(acq, n_cand, BO_CAND_GRID, nullptr, nullptr, nullptr, 1, cand_offset, nullptr, 0,
+                     topq, top_val, top_idx, ws, ws_bytes, (hipStream_t)stream, &h, n_obj,
+                     (const unsigned int*)mask);
 }
 
 int bo_pareto_mask(const double* y, int64_t n, int32_t n_obj, uint8_t* mask, void* stream) {

@@ -70,10 +70,12 @@ def build(verbose=True, jobs=None):
     objs = [o for o, _ in results]
     rebuilt = any(r for _, r in results)
     if rebuilt or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+        tmp = LIB + ".tmp"      # linked aside, then renamed: a reader never sees a partial file
+        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
         if verbose:
             print(f"built {LIB}")
     return LIB

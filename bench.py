@@ -567,6 +567,9 @@ def main():
     ap.add_argument("--acq", choices=("sum_ucb", "hvi"), default="sum_ucb",
                     help="sum_ucb = the reference's 'hypervolume improvement' (sum of UCBs, fused top-q); "
                          "hvi = exact hypervolume improvement over the evaluated Pareto front (extension)")
+    ap.add_argument("--hvi-unmasked", action="store_true",
+                    help="--acq hvi: exclude the evaluated points per call (hash set) instead of the "
+                         "persistent exclusion mask")
     args = ap.parse_args()
     if args.mode is None:
         args.mode = "fp32" if args.config == "C5" else "auto"
@@ -677,23 +680,43 @@ def main():
         scale = (ctypes.c_double * n_obj)(*np.sqrt(pv[:n_obj]))
         strm = bo.device.stream_handle(dev)
         n_boxes = [0]
+        # the evaluated points' exclusion mask of this shard (bo_excl_mask_update), as the loop
+        # keeps it: built once, then extended by each iteration's q new points (both timed here,
+        # outside the step; reported in hvi_select)
+        from bayesopt_smart_amd.acquisition import ExclusionMask
+        hvi_mask = ExclusionMask(cands, offset, per_rank, dev)
+        mask_ms = {}
+        for tag, rows in (("build_ms", x[:-q]), ("extend_q_ms", x)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            hvi_mask.update(rows)
+            e1.record()
+            torch.cuda.synchronize()
+            mask_ms[tag] = e0.elapsed_time(e1)
 
         def step_hvi():
             # fused predict writing the UCB arrays, the box decomposition of the non-dominated
             # region (host), then ONE pass computing the exact HVI of every candidate and its
-            # top-q with exclusion (bo_hvi_select_topq), event-timed
+            # top-q with exclusion (bo_hvi_select_topq_masked over the shard's exclusion mask;
+            # --hvi-unmasked: bo_hvi_select_topq with the points), event-timed
             bo.predict_acquire(xd, yd, kd, cands, pm, pv, ls, betas, outputs=outputs, topq=0,
                                offset=offset, count=per_rank, out=out, device=dev, mode=args.mode)
             boxes = torch.as_tensor(hypervolume_boxes(front_y, ref_pt), device=dev)
             n_boxes[0] = boxes.shape[0]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            bo._lib.check(lib.bo_hvi_select_topq(
-                out["acq"].data_ptr(), out["ucb"].data_ptr(), per_rank, per_rank, n_obj, shift, scale,
-                boxes.data_ptr(), boxes.shape[0], cands.kind_code,
-                (cands.tensor[offset:].data_ptr() if cands.kind in ("i64", "f64") else cands.cand_arg),
-                glo, gsh, cands.dim, offset, exd.data_ptr(), exd.shape[0], q, rec.data_ptr(),
-                rec.data_ptr() + 8 * q, sel_ws.data_ptr(), sel_ws.numel(), strm), "hvi_select")
+            if args.hvi_unmasked:
+                bo._lib.check(lib.bo_hvi_select_topq(
+                    out["acq"].data_ptr(), out["ucb"].data_ptr(), per_rank, per_rank, n_obj, shift, scale,
+                    boxes.data_ptr(), boxes.shape[0], cands.kind_code,
+                    (cands.tensor[offset:].data_ptr() if cands.kind in ("i64", "f64") else cands.cand_arg),
+                    glo, gsh, cands.dim, offset, exd.data_ptr(), exd.shape[0], q, rec.data_ptr(),
+                    rec.data_ptr() + 8 * q, sel_ws.data_ptr(), sel_ws.numel(), strm), "hvi_select")
+            else:
+                bo._lib.check(lib.bo_hvi_select_topq_masked(
+                    out["acq"].data_ptr(), out["ucb"].data_ptr(), per_rank, per_rank, n_obj, shift, scale,
+                    boxes.data_ptr(), boxes.shape[0], offset, hvi_mask.ptr, q, rec.data_ptr(),
+                    rec.data_ptr() + 8 * q, sel_ws.data_ptr(), sel_ws.numel(), strm), "hvi_select_masked")
             e1.record()
             hvi_ev.append((e0, e1))
 
@@ -848,6 +871,9 @@ def main():
             res["hvi_select"] = {"kernels": (f"select_small_kernel<{n_obj}, 4> + select_merge_kernel<4>" if q <= 4 else
                                              f"select_stream_kernel<{n_obj}, 4> + bo_topq_merge_kernel")
                                             + " (exact HVI + top-q, one pass)",
+                                 "exclusion": ("per-call hash set of the points (bo_hvi_select_topq)" if args.hvi_unmasked
+                                               else "persistent exclusion mask (bo_hvi_select_topq_masked)"),
+                                 "excl_mask": None if args.hvi_unmasked else mask_ms,
                                  "ms": hms, "n_boxes": n_boxes[0], "front_points": int(front_y.shape[0]),
                                  "bytes_per_candidate": 8 * n_obj + 8,
                                  "achieved_GBps": hb / (hms * 1e-3) / 1e9,
@@ -892,48 +918,74 @@ def main():
 def standalone_select(lib, bo, acq, cands, offset, n, xd, q, dev, fused_sel, reps=20):
     """bo_select_topq (select_next_batch over a stored acquisition array, acquisition.py:116-144)
     on this shard's acq array from the timed run, with the evaluated points excluded: device time
-    per call (one-pass selection kernel + the final merge, HIP-graph replayed), its HBM rate on the 8 B per
-    candidate it must read, and whether it selects what the fused kernel selected.  Outside the
-    timed region."""
+    per call (one-pass selection kernel + the final merge, HIP-graph replayed), its HBM rate on the
+    8 B per candidate it must read, and whether it selects what the fused kernel selected.  `ms`
+    is the masked call (bo_select_topq_masked over the shard's persistent exclusion mask, which
+    the loop builds once and extends by q points per iteration -- both timed, `excl_mask`);
+    `per_call_exclusion` the same selection with the points' hash set built inside the call
+    (bo_select_topq).  Outside the timed region."""
     import ctypes
     import torch
+    from bayesopt_smart_amd.acquisition import ExclusionMask
     ws = torch.empty(lib.bo_select_topq_workspace_size(n, q), dtype=torch.uint8, device=dev)
     tv = torch.empty(q, dtype=torch.float64, device=dev)
     ti = torch.empty(q, dtype=torch.int64, device=dev)
     glo = (ctypes.c_int64 * 8)(*((list(cands.lo) if cands.lo else []) + [0] * (8 - len(cands.lo or []))))
     gsh = (ctypes.c_int64 * 8)(*((list(cands.shape) if cands.shape else []) + [1] * (8 - len(cands.shape or []))))
     carg = cands.tensor[offset:].data_ptr() if cands.kind in ("i64", "f64") else cands.cand_arg
+    xh = xd.cpu().numpy()
+    mask = ExclusionMask(cands, offset, n, dev)
+    mask_ms = {}
+    for tag, rows in (("build_ms", xh[:-q]), ("extend_q_ms", xh)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        mask.update(rows)
+        e1.record()
+        torch.cuda.synchronize()
+        mask_ms[tag] = e0.elapsed_time(e1)
 
-    def call(strm):
+    def call_points(strm):
         bo._lib.check(lib.bo_select_topq(acq.data_ptr(), n, cands.kind_code, carg, glo, gsh, cands.dim,
                                          offset, xd.data_ptr(), xd.shape[0], q, tv.data_ptr(),
                                          ti.data_ptr(), ws.data_ptr(), ws.numel(), strm), "select")
-    call(bo.device.stream_handle(dev))
-    torch.cuda.synchronize()
-    got = ti.cpu().numpy()
-    # the reps calls replayed as one HIP graph: device time per call, no host launch cost
-    side = torch.cuda.Stream(dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(side):
-        call(side.cuda_stream)
-        with torch.cuda.graph(g, stream=side):
-            for _ in range(reps):
-                call(side.cuda_stream)
-    torch.cuda.current_stream(dev).wait_stream(side)
-    g.replay()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+
+    def call_masked(strm):
+        bo._lib.check(lib.bo_select_topq_masked(acq.data_ptr(), n, offset, mask.ptr, q, tv.data_ptr(),
+                                                ti.data_ptr(), ws.data_ptr(), ws.numel(), strm), "select_masked")
+
+    def timed(call):
+        call(bo.device.stream_handle(dev))
+        torch.cuda.synchronize()
+        got = ti.cpu().numpy()
+        # the reps calls replayed as one HIP graph: device time per call, no host launch cost
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            call(side.cuda_stream)
+            with torch.cuda.graph(g, stream=side):
+                for _ in range(reps):
+                    call(side.cuda_stream)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps, bool(np.array_equal(got[got >= 0], np.asarray(fused_sel)))
+
+    ms_p, ok_p = timed(call_points)
+    ms, ok = timed(call_masked)
     return {"kernels": ("select_small_kernel<0, 4> + select_merge_kernel<4>" if q <= 4 else
                         "select_stream_kernel<0, 8> + bo_topq_merge_kernel") + " (HIP-graph replay)",
+            "exclusion": "persistent exclusion mask (bo_select_topq_masked)",
             "ms": ms, "bytes": 8 * n, "achieved_GBps": 8 * n / (ms * 1e-3) / 1e9,
             "hbm_frac": 8 * n / (ms * 1e-3) / 1e9 / 8000.0,
-            "matches_fused_selection": bool(np.array_equal(got[got >= 0], np.asarray(fused_sel)))}
+            "excl_mask": mask_ms,
+            "per_call_exclusion": {"ms": ms_p, "matches_fused_selection": ok_p},
+            "matches_fused_selection": ok and ok_p}
 
 
 def _rows_in(pts, x):

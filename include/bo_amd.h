@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define BO_ABI_VERSION 4
+#define BO_ABI_VERSION 5
 #define BO_MAX_OBJ 8      /* objectives per call                              */
 #define BO_MAX_DIM 8      /* input dimensions                                 */
 #define BO_MAX_TOPQ 48    /* batch size of the fused top-q selection          */
@@ -208,6 +208,31 @@ int bo_select_topq(const double* acq, int64_t n_cand, int32_t cand_kind, const v
                    void* stream);
 size_t bo_select_topq_workspace_size(int64_t n_cand, int32_t topq);
 
+/* The exclusion of acquisition.py:137-139 ("candidate equal in every coordinate to an evaluated
+ * point") as a candidate bit mask, kept across iterations (ABI 5).  The evaluated set grows by
+ * q points per iteration, so the mask is built once and then extended by the new rows only.
+ *
+ * bo_excl_mask_update: sets bit j (word j / 32, bit j % 32) of `mask` (device, bo_excl_mask_bytes
+ * (n_cand)) for every local candidate j (global index cand_offset + j) equal to one of the rows
+ * excl_points[first_excl .. n_excl) (device [n_excl][dim]); clear != 0 zeroes the mask first.
+ * Candidates as bo_select_topq's.  Grid candidates: one thread per point, the grid index found
+ * arithmetically.  Other kinds: a hash set of the new rows in `workspace`
+ * (bo_excl_mask_workspace_size(n_excl - first_excl) bytes; unused for a grid) and one pass over
+ * the candidates.
+ * bo_select_topq_masked / bo_hvi_select_topq_masked: bo_select_topq / bo_hvi_select_topq with
+ * the mask in place of the points: an excluded element is dropped as it is loaded (no hash build,
+ * no probes).  Same results as the unmasked calls given the same evaluated points. */
+size_t bo_excl_mask_bytes(int64_t n_cand);
+size_t bo_excl_mask_workspace_size(int64_t n_excl);
+int bo_excl_mask_update(uint32_t* mask, int64_t n_cand, int32_t cand_kind, const void* cand,
+                        const int64_t* grid_lo, const int64_t* grid_shape, int32_t dim,
+                        int64_t cand_offset, const double* excl_points, int64_t first_excl,
+                        int64_t n_excl, int32_t clear, void* workspace, size_t workspace_bytes,
+                        void* stream);
+int bo_select_topq_masked(const double* acq, int64_t n_cand, int64_t cand_offset,
+                          const uint32_t* mask, int32_t topq, double* top_val, int64_t* top_idx,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
 /* is_pareto_efficient  bayesopt/pareto.py:12-45: mask[i] = 1 iff no row j dominates row i
  * (maximisation, weak dominance; NaN rows never dominate nor are dominated).
  * y: device [n][n_obj] row-major; mask: device uint8 [n]. Bit-exact. */
@@ -239,6 +264,12 @@ int bo_hvi_select_topq(double* acq, const double* ucb, int64_t ld, int64_t n_can
                        const int64_t* grid_shape, int32_t dim, int64_t cand_offset,
                        const double* excl_points, int64_t n_excl, int32_t topq, double* top_val,
                        int64_t* top_idx, void* workspace, size_t workspace_bytes, void* stream);
+int bo_hvi_select_topq_masked(double* acq, const double* ucb, int64_t ld, int64_t n_cand,
+                              int32_t n_obj, const double* shift, const double* scale,
+                              const double* boxes, int64_t n_boxes, int64_t cand_offset,
+                              const uint32_t* mask, int32_t topq, double* top_val,
+                              int64_t* top_idx, void* workspace, size_t workspace_bytes,
+                              void* stream);
 /* bo_box_volume_sum: out[0] (device) = sum_b prod_k max(0, min(upper_bk, upper[k]) - lower_bk)
  * over `boxes` (device, bo_hvi_boxes layout): the volume of the boxes clipped above at `upper`
  * (host [n_obj]).  With the boxes of the region a front does NOT dominate and upper = the

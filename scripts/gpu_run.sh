@@ -4,6 +4,8 @@
 #   scripts/gpu_run.sh TAG step [step ...]
 #   steps: tests[:<pytest selection>]  smoke  bench[:<bench args>]  iter:<cfg>  fit:<cfg>
 #          prof:<bench args>  (rocprofv3 --kernel-trace --stats of bench.py)
+#          py:<script args>  pyprof:<script args> (rocprofv3 of a python script)
+#          env:VAR=value (exported for the following steps; env:VAR= unsets it)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 TAG=$1; shift
@@ -39,6 +41,16 @@ for st in "$@"; do
           python "$R/bench.py" $arg > "$R/$OUT/prof_$i.log" 2>&1 ); rc=$?
       echo "[$i] rocprof $arg rc=$rc"; tail -2 "$OUT/prof_$i.log"
       f=$(find "$OUT/prof_$i" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -12 "$f" | cut -c1-200 ;;
+    env)
+      arg=${arg//@R@/$R}
+      if [ -z "${arg#*=}" ]; then unset "${arg%%=*}"; else export "$arg"; fi
+      echo "[$i] env $arg"; rc=0 ;;
+    pyprof)
+      export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/pyprof_$i" -o run -- \
+          python $(cd "$R" && echo "$R/$arg") > "$R/$OUT/pyprof_$i.log" 2>&1 ); rc=$?
+      echo "[$i] rocprof python $arg rc=$rc"; tail -3 "$OUT/pyprof_$i.log"
+      f=$(find "$OUT/pyprof_$i" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -12 "$f" | cut -c1-200 ;;
     py)
       timeout -k 10 600 python $arg > "$OUT/py_$i.log" 2>&1; rc=$?
       echo "[$i] python $arg rc=$rc"; tail -20 "$OUT/py_$i.log" ;;

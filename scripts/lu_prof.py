@@ -11,6 +11,10 @@ cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "C3"]
 ls_fit = float(sys.argv[2]) if len(sys.argv) > 2 else 680.0
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 x, y, pm, pv, ls, betas, _, _ = bench.make_config_problem(cfg, 1)
+if len(sys.argv) > 4 and int(sys.argv[4]) > x.shape[0]:       # N above the config's: extra grid points
+    extra = np.random.default_rng(5).choice(1024 * 1024, size=int(sys.argv[4]) - x.shape[0], replace=False)
+    xe = np.stack([extra // 1024, extra % 1024], 1).astype(np.float64)
+    x = np.concatenate([x, xe if x.shape[1] == 2 else np.resize(xe, (xe.shape[0], x.shape[1]))])
 n, n_obj = x.shape[0], len(pm)
 dev = torch.device("cuda", 0)
 xd = torch.tensor(x, device=dev)

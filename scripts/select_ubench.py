@@ -4,7 +4,8 @@ the figure), with the evaluated points excluded; checked against numpy's order.
 
     python scripts/select_ubench.py [--cases C3,C5] [--reps 50]
 
-One JSON line per case: us per call (selection kernel + final merge), GB/s on the 8 B per
+One JSON line per case and exclusion form (points: the per-call hash set, bo_select_topq;
+masked: the persistent exclusion mask, bo_select_topq_masked): us per call (selection kernel + final merge), GB/s on the 8 B per
 candidate read, fraction of 8 TB/s.
 """
 import argparse
@@ -33,7 +34,7 @@ CASES = {  # name: (grid side0, side1, n evaluated, q)
 }
 
 
-def run(name, reps):
+def run(name, reps, masked=False):
     s0, s1, n_ev, q = CASES[name]
     m = s0 * s1
     rng = np.random.default_rng(1)
@@ -51,8 +52,16 @@ def run(name, reps):
     glo = (ctypes.c_int64 * 8)(*([0] * 8))
     gsh = (ctypes.c_int64 * 8)(*([s0, s1] + [1] * 6))
 
+    cands = bo.predict.CandidateSet.grid([(0, s0), (0, s1)])
+    mask = bo.acquisition.ExclusionMask(cands, 0, m, dev).update(ev)
+
     def call():
-        _lib.check(lib.bo_select_topq(acq.data_ptr(), m, bo.predict.CandidateSet.grid([(0, s0), (0, s1)]).kind_code,
+        if masked:
+            _lib.check(lib.bo_select_topq_masked(acq.data_ptr(), m, 0, mask.ptr, q, tv.data_ptr(), ti.data_ptr(),
+                                                 ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream),
+                       "select_masked")
+            return
+        _lib.check(lib.bo_select_topq(acq.data_ptr(), m, cands.kind_code,
                                       None, glo, gsh, 2, 0, xd.data_ptr(), n_ev, q, tv.data_ptr(),
                                       ti.data_ptr(), ws.data_ptr(), ws.numel(),
                                       torch.cuda.current_stream().cuda_stream), "select")
@@ -80,7 +89,7 @@ def run(name, reps):
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    print(json.dumps({"case": name, "n_cand": m, "n_excl": n_ev, "q": q, "us_per_call": round(us, 2),
+    print(json.dumps({"case": name, "masked": masked, "n_cand": m, "n_excl": n_ev, "q": q, "us_per_call": round(us, 2),
                       "GBps": round(8 * m / (us * 1e-6) / 1e9, 1),
                       "hbm_frac": round(8 * m / (us * 1e-6) / 1e9 / 8000.0, 4), "matches_numpy": ok}),
           flush=True)
@@ -92,7 +101,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     args = ap.parse_args()
     for c in args.cases.split(","):
-        run(c, args.reps)
+        for masked in (False, True):
+            run(c, args.reps, masked)
 
 
 if __name__ == "__main__":

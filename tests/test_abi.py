@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_status_strings_and_version():
     from bayesopt_smart_amd import _lib
     lib = _lib.load()
-    assert lib.bo_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.bo_abi_version() == _lib.ABI_VERSION == 5
     assert lib.bo_status_string(_lib.ERR_NOT_PD) == b"Matrix is not positive definite"
     with pytest.raises(np.linalg.LinAlgError):
         _lib.check(_lib.ERR_SINGULAR, "x")

@@ -130,14 +130,15 @@ def test_device_hvi_full_scan_properties():
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,m,q", [("grid", 2, 3), ("grid", 3, 16), ("f64", 2, 8), ("sobol", 3, 5),
                                       ("grid", 2, 20), ("sobol", 2, 48)])
-def test_fused_hvi_select_matches_scan_plus_oracle_select(kind, m, q):
+@pytest.mark.parametrize("masked", [False, True])
+def test_fused_hvi_select_matches_scan_plus_oracle_select(kind, m, q, masked):
     """bo_hvi_select_topq (exact HVI and its top-q in one pass) writes the same acquisition
     array as the standalone HVI scan, bit for bit, and selects what select_next_batch
     (acquisition.py:116-144, the oracle's deterministic order) selects over it, evaluated
-    points skipped (hash set of the evaluated points, exact coordinates), for q up to
-    BO_MAX_TOPQ."""
+    points skipped (hash set of the evaluated points, exact coordinates; or, `masked`, the
+    persistent ExclusionMask -- bo_hvi_select_topq_masked), for q up to BO_MAX_TOPQ."""
     import torch
-    from bayesopt_smart_amd.acquisition import hvi_select_indices, hypervolume_improvement_exact
+    from bayesopt_smart_amd.acquisition import ExclusionMask, hvi_select_indices, hypervolume_improvement_exact
     from bayesopt_smart_amd.predict import CandidateSet
     rng = np.random.default_rng(m * 100 + q)
     if kind == "grid":
@@ -154,7 +155,10 @@ def test_fused_hvi_select_matches_scan_plus_oracle_select(kind, m, q):
     ev = cands.points(rng.choice(n, 40, replace=False)).astype(np.float64)
     ref_pt = np.full(m, -4.0)
     acq = torch.zeros(n, dtype=torch.float64, device="cuda")
-    idx = hvi_select_indices(acq, ucb, y, 40, ref_pt, pm, pv, cands, ev, q)
+    mask = None
+    if masked:                      # built in two steps, as the loop extends it
+        mask = ExclusionMask(cands, 0, n, "cuda").update(ev[:25])
+    idx = hvi_select_indices(acq, ucb, y, 40, ref_pt, pm, pv, cands, ev, q, mask=mask)
     front = y[O.is_pareto_efficient(y)]
     scan = hypervolume_improvement_exact(ucb, front, ref_pt, pm, pv).cpu().numpy()
     np.testing.assert_array_equal(acq.cpu().numpy(), scan)
