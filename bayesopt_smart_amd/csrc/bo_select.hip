@@ -694,6 +694,36 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
   };
   // the first span's loads go out before the hash build (they need no table)
   if (b_first < a.n_cand) load_span(b_first, run);
+  if (a.n_excl == 0) {
+    // lean form: nothing to probe (the exclusion mask dropped the evaluated points at load, or
+    // there are none); a lane keeps the best U of all its spans, then the rounds
+    if (b_first >= a.n_cand) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) { run.k[u] = 0ull; run.i[u] = -1; }
+    }
+    run.sort();
+    for (long long s0 = b_first + b_stride; s0 < a.n_cand; s0 += b_stride) {   // workgroup-uniform
+      LaneRun<U> nx;
+      load_span(s0, nx);
+      nx.sort();
+      lane_keep_best<U>(run, nx);
+    }
+#ifdef BO_SEL_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    SEL_STAMP(1);
+    double ov;
+    long long oi;
+    const bool w0 = block_topq_rounds<U>(run, q, 16, wl, ov, oi);
+    if (w0 && lane < q) a.partial[(size_t)blockIdx.x * q + lane] = TopEntry{ov, oi};
+#ifdef BO_SEL_TIMING
+    SEL_STAMP(2);
+    if ((blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && threadIdx.x == 0)
+      printf("lean sel block %d: loads %lld rounds %lld ticks (x10 ns)\n", (int)blockIdx.x, _t[1] - _t[0],
+             _t[2] - _t[1]);
+#endif
+    return;
+  }
   if (a.lds_slots > 0) {
     int* lidx = (int*)(lkeys + a.lds_slots);
     for (int t = tid; t < a.lds_slots; t += blockDim.x) lkeys[t] = 0ull;
@@ -729,107 +759,6 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
     printf("sel block %d wave %d: hash %lld loads %lld span %lld merge %lld ticks (x10 ns)\n", (int)blockIdx.x,
            (int)(threadIdx.x >> 6), _t[1] - _t[0], _t[2] - _t[1], _t[3] - _t[2], _t[4] - _t[3]);
 #endif
-}
-
-// The lean selection (nothing to probe: the exclusion mask, or no evaluated points), q <= 4, on
-// NW = 4 waves per workgroup (one per SIMD) with UL = 16 elements per lane: each lane keeps the
-// best 4 of its elements (4 sorted runs of 4, bitonic merges), then q arg-best rounds per wave and
-// q more in wave 0 (block_topq_rounds).  The rounds are VALU work, so fewer waves holding more
-// elements each cut them: 16 waves x 4 elements per CU ran them 4x per SIMD (C3: select 12.4 us,
-// HVI + select 27 us).  All of a lane's loads (UL acquisition values, or UL x M UCB values) are
-// issued before any is used.  M >= 1: the exact HVI of each element written to acq first, the box
-// loop outside the element loop in runs of 4 (the standalone scan's summation order).
-constexpr int kLeanNW = 4, kLeanU = 16;
-
-template <int M>
-__global__ __launch_bounds__(64 * kLeanNW) void select_lean_kernel(SelArgs a, HviIn h) {
-  __shared__ TopEntry wl[kLeanNW * 4];
-  constexpr int U = kLeanU, NR = U / 4;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = a.topq;
-  const long long span = 64LL * kLeanNW * U;
-  LaneRun<4> keep;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) { keep.k[u] = 0ull; keep.i[u] = -1; }
-  for (long long s0 = (long long)blockIdx.x * span; s0 < a.n_cand; s0 += (long long)gridDim.x * span) {
-    const long long jw = s0 + (long long)wave * 64 * U + lane;     // element u: jw + 64 u
-    double v[U];
-    if constexpr (M == 0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long long j = jw + 64 * u;
-        v[u] = j < a.n_cand ? __builtin_nontemporal_load(a.acq + j) : 0.0;
-      }
-    } else {
-      double p[U][M];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long long j = jw + 64 * u;
-#pragma unroll
-        for (int k = 0; k < M; ++k) p[u][k] = j < a.n_cand ? h.ucb[(long long)k * h.ld + j] : 0.0;
-      }
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        double hv[4];
-        bool nan[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          hv[e] = 0.0;
-          nan[e] = false;
-#pragma unroll
-          for (int k = 0; k < M; ++k) {
-            p[4 * r + e][k] = __builtin_fma(h.scale[k], p[4 * r + e][k], h.shift[k]);
-            nan[e] = nan[e] || (p[4 * r + e][k] != p[4 * r + e][k]);
-          }
-        }
-        const double* b = h.boxes;
-        for (long long t = 0; t < h.n_boxes; ++t, b += 2 * M) {
-          double lo[M], up[M];
-#pragma unroll
-          for (int k = 0; k < M; ++k) { lo[k] = b[k]; up[k] = b[M + k]; }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            double w = 1.0;
-#pragma unroll
-            for (int k = 0; k < M; ++k) {
-              const double hi2 = p[4 * r + e][k] < up[k] ? p[4 * r + e][k] : up[k];
-              w *= fmax(hi2 - lo[k], 0.0);
-            }
-            hv[e] += w;
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const long long j = jw + 64 * (4 * r + e);
-          v[4 * r + e] = nan[e] ? __builtin_nan("") : hv[e];
-          if (j < a.n_cand) h.acq_out[j] = v[4 * r + e];
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      LaneRun<4> run;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const long long j = jw + 64 * (4 * r + e);
-        const bool ok = j < a.n_cand && !xbit(a.xbits, j);
-        run.i[e] = ok ? a.cand_offset + j : -1;
-        run.k[e] = ok ? bo_order_key(v[4 * r + e], 0) : 0ull;
-      }
-      run.sort();
-      lane_keep_best<4>(keep, run);
-    }
-  }
-  double ov;
-  long long oi;
-  if (block_topq_rounds<4>(keep, q, kLeanNW, wl, ov, oi) && lane < q)
-    a.partial[(size_t)blockIdx.x * q + lane] = TopEntry{ov, oi};
-}
-
-template <int M>
-int launch_select_lean(const SelArgs& a, const HviIn& h, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL(select_lean_kernel<M>, dim3(blocks), dim3(64 * kLeanNW), 0, s, a, h);
-  BO_CHECK_HIP(hipGetLastError());
-  return BO_OK;
 }
 
 // Final merge of n_lists <= 1024 sorted top-q lists ([n_lists][q], q <= 4): one workgroup, a lane
@@ -1300,21 +1229,18 @@ int select_impl(const double* acq, int64_t n_cand, int32_t kind, const void* can
   const HviIn& hv = h ? *h : hz;
   int st;
   if (topq <= kSmallQ) {
-    // lean (nothing to probe): 4-wave workgroups of 64 x 4 x 16 elements, at most one per CU;
-    // otherwise one span (16 waves x 64 U elements) per workgroup, one workgroup per CU.
-    // [blocks][q] lists either way
-    const bool lean = a.n_excl == 0;
-    const long long per_block = lean ? 64LL * kLeanNW * kLeanU : 16LL * 64 * (m == 0 ? kSmallU0 : kSmallUM);
+    // one span (16 waves x 64 U elements) per workgroup, one workgroup per CU; [blocks][q] lists
+    const long long per_block = 16LL * 64 * (m == 0 ? kSmallU0 : kSmallUM);
     long long blocks = (n_cand + per_block - 1) / per_block;
     const int max_blocks = cus_count() < 1024 ? cus_count() : 1024;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
     switch (m) {
-      case 0: st = lean ? launch_select_lean<0>(a, hv, (int)blocks, s) : launch_select_small<0>(a, hv, (int)blocks, s); break;
-      case 1: st = lean ? launch_select_lean<1>(a, hv, (int)blocks, s) : launch_select_small<1>(a, hv, (int)blocks, s); break;
-      case 2: st = lean ? launch_select_lean<2>(a, hv, (int)blocks, s) : launch_select_small<2>(a, hv, (int)blocks, s); break;
-      case 3: st = lean ? launch_select_lean<3>(a, hv, (int)blocks, s) : launch_select_small<3>(a, hv, (int)blocks, s); break;
-      case 4: st = lean ? launch_select_lean<4>(a, hv, (int)blocks, s) : launch_select_small<4>(a, hv, (int)blocks, s); break;
+      case 0: st = launch_select_small<0>(a, hv, (int)blocks, s); break;
+      case 1: st = launch_select_small<1>(a, hv, (int)blocks, s); break;
+      case 2: st = launch_select_small<2>(a, hv, (int)blocks, s); break;
+      case 3: st = launch_select_small<3>(a, hv, (int)blocks, s); break;
+      case 4: st = launch_select_small<4>(a, hv, (int)blocks, s); break;
       default: return BO_ERR_UNSUPPORTED;
     }
     if (st != BO_OK) return st;
