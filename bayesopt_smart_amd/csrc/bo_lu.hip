@@ -84,7 +84,12 @@ __device__ long long bo_lu_cstamp[64 * LB_DIAG * 4];
 struct LuGeo {
   int n, n_p, nbs;              // N, N padded to 16, strips
   long long Na;                 // leading dimension (= n_p)
+  int small_panel;              // 1: factor a strip of <= SP_ROWS rows on SPW waves (panel_small)
 };
+
+constexpr int SPW = 2;                  // waves of the small panel
+constexpr int SPR = 4;                  // its rows per lane
+constexpr int SP_ROWS = SPW * 64 * SPR; // 512
 
 struct LuBatch {                // one factorisation per slot (the objectives whose Cholesky failed)
   double* A[BO_MAX_OBJ];
@@ -373,6 +378,141 @@ __device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const 
   __syncthreads();                                   // L.T is rewritten by the next phase
 }
 
+// The panel of strip k when its rows to factor (16 k .. n_p) number at most SP_ROWS: they move
+// through LDS (P, column-major) from the workgroup's 8 waves to SPW = 2 waves, SPR = 4 rows per
+// lane in registers (row offset o = 256 wave + 64 r + lane), the other waves end, and each pivot
+// column synchronises two waves instead of eight.  The arithmetic is the 8-wave loop's, operation
+// for operation (the same pivot order, reciprocal and FMAs: bit-identical factors); the rows of
+// step k-1's U block (base .. 16 k) are stored by their threads before the hand-off.
+template <int LR>
+__device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, double* __restrict__ P,
+                            const double (&w)[LR][LB], int base, long long c0, double* __restrict__ A,
+                            int* __restrict__ prec, int slot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int top = LB * k, R = g.n_p - top;
+#pragma unroll
+  for (int r = 0; r < LR; ++r) {
+    const long long row = own_row(base, r);
+    if (row >= top && row < g.n_p) {
+#pragma unroll
+      for (int c = 0; c < LB; ++c) P[c * SP_ROWS + (row - top)] = w[r][c];
+    } else if (row < top) {
+#pragma unroll
+      for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + row] = w[r][c];
+    }
+  }
+  __syncthreads();
+  if (wave >= SPW) return;                   // s_barrier then counts the SPW waves left
+  double v[SPR][LB];
+  int off[SPR];
+#pragma unroll
+  for (int r = 0; r < SPR; ++r) {
+    off[r] = wave * 64 * SPR + 64 * r + lane;
+#pragma unroll
+    for (int c = 0; c < LB; ++c) v[r][c] = off[r] < R ? P[c * SP_ROWS + off[r]] : 0.0;
+  }
+  bool singular = false;
+  // rolled, with the rows rotated as in the 8-wave loop (lu_step_kernel)
+#pragma unroll 1
+  for (int j = 0; j < LB; ++j) {
+    const int bf = j & 1;
+    LU_CSTAMP(k, j, 0);
+    unsigned long long bk = 0ull;
+    int bo = 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < SPR; ++r) {
+      const unsigned long long kr = piv_key(v[r][0], off[r] >= j && off[r] < R);
+      if (kr > bk) { bk = kr; bo = off[r]; }                   // first max per lane
+    }
+    unsigned long long wk;
+    int wo;
+    piv_wave_best(bk, bo, wk, wo);
+    LU_CSTAMP(k, j, 1);
+#pragma unroll
+    for (int r = 0; r < SPR; ++r)
+      if (wk != 0ull && off[r] == wo) {
+#pragma unroll
+        for (int c = 0; c < LB; c += 2) *(d2*)&L.cand[bf][wave][c] = (d2){v[r][c], v[r][c + 1]};
+      }
+    if (lane == 0) {
+      L.ck[bf][wave] = wk;
+      L.cr[bf][wave] = wk != 0ull ? wo : 0x7fffffff;
+    }
+    if (wave == 0 && lane == j) {                              // row 16 k + j: offset j, slot 0
+#pragma unroll
+      for (int c = 0; c < LB; c += 2) *(d2*)&L.grow[bf][c] = (d2){v[0][c], v[0][c + 1]};
+    }
+    __syncthreads();
+    LU_CSTAMP(k, j, 2);
+    const unsigned long long k0 = L.ck[bf][0], k1 = L.ck[bf][1];
+    const int r0 = L.cr[bf][0], r1 = L.cr[bf][1];
+    const bool t1 = piv_before(k1, r1, k0, r0);
+    const unsigned long long pk = t1 ? k1 : k0;
+    int po = t1 ? r1 : r0, pw = t1 ? 1 : 0;
+    if (pk <= 1ull) { singular = true; po = j; pw = -1; }       // zero / NaN column: no swap
+    const double* prow = pw >= 0 ? L.cand[bf][pw] : L.grow[bf];
+    if (tid == 0) L.piv[j] = top + po;
+    double pr[LB];
+#pragma unroll
+    for (int c = 0; c < LB; c += 2) {
+      const d2 x = *(const d2*)(prow + c);
+      pr[c] = x.x;
+      pr[c + 1] = x.y;
+    }
+    const double rp = 1.0 / pr[0];
+    const int live = LB - j;
+    double l[SPR];
+    bool act[SPR];
+#pragma unroll
+    for (int r = 0; r < SPR; ++r) {
+      if (off[r] == j) {
+#pragma unroll
+        for (int c = 0; c < LB; ++c) v[r][c] = pr[c];
+      } else if (off[r] == po) {
+#pragma unroll
+        for (int c = 0; c < LB; c += 2) {
+          const d2 x = *(const d2*)&L.grow[bf][c];
+          v[r][c] = x.x;
+          v[r][c + 1] = x.y;
+        }
+      }
+      act[r] = off[r] > j && off[r] < R;
+      l[r] = v[r][0] * rp;
+      if (act[r]) v[r][0] = l[r];
+    }
+#pragma unroll
+    for (int c = 1; c < LB; ++c)
+      if (c < live) {
+#pragma unroll
+        for (int r = 0; r < SPR; ++r)
+          if (act[r]) v[r][c] = __builtin_fma(-l[r], pr[c], v[r][c]);
+      }
+#pragma unroll
+    for (int r = 0; r < SPR; ++r) {
+      const double t = v[r][0];
+#pragma unroll
+      for (int c = 0; c + 1 < LB; ++c) v[r][c] = v[r][c + 1];
+      v[r][LB - 1] = t;
+    }
+    LU_CSTAMP(k, j, 3);
+  }
+  if (tid == 0 && singular) bt.status[slot] = 1;
+  LU_STAMP(k, 3);
+  if (wave == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       // L.piv (lane 0) to the wave
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    build_perm(L, k, prec + (long long)k * PREC);
+  }
+  LU_STAMP(k, 4);
+#pragma unroll
+  for (int r = 0; r < SPR; ++r)
+    if (off[r] < R) {
+#pragma unroll
+      for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + top + off[r]] = v[r][c];
+    }
+}
+
 // Launch k: block 0 = panel (strip k), blocks 1.. = strips k + 1 .. (update of step k-1);
 // grid y = the batch slot.
 template <int LR>
@@ -402,6 +542,17 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
   }
   if (k > 0) strip_apply(A, g, prec + (long long)(k - 1) * PREC, k - 1, L, w);
   if (stamp) LU_STAMP(k, 2);
+  // the small panel only where the 8-wave loop holds two rows per thread (N_p in (512, 1024]):
+  // at N = 1024 3.84 -> 3.43 ms per inverse; at N = 512 (one row per thread) it measured 1.40 vs
+  // 1.36 ms (same box) -- the per-column latency (~1.5 us: pivot search, two LDS round trips, the
+  // division, the update) is the same on 2 waves as on 8
+  if constexpr (LR == 2) {
+    __shared__ double P[LB * SP_ROWS];         // the small panel's hand-off (64 KB)
+    if (blockIdx.x == 0 && g.small_panel && g.n_p - LB * k <= SP_ROWS) {   // workgroup-uniform
+      panel_small<LR>(bt, g, k, L, P, w, base, c0, A, prec, slot);
+      return;
+    }
+  }
   if (blockIdx.x == 0) {
     // factor strip k: columns j, pivot rows g0 = 16 k + j.  A ROLLED loop (the unrolled one was
     // ~60 KB of code run once per launch: instruction fetch, not arithmetic, set its 36 us), so
@@ -905,6 +1056,12 @@ LuGeo make_lu_geo(int n) {
   g.n_p = (n + LB - 1) / LB * LB;
   g.nbs = g.n_p / LB;
   g.Na = g.n_p;
+  // BO_LU_PANEL=wide: every panel on the 8-wave loop (A/B only)
+  static const int small = [] {
+    const char* e = getenv("BO_LU_PANEL");
+    return (e && strcmp(e, "wide") == 0) ? 0 : 1;
+  }();
+  g.small_panel = small;
   return g;
 }
 
