@@ -660,7 +660,8 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
         hv[u] = 0.0;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
-          p[u][k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
+          p[u][k] = __builtin_fma(h.scale[k], in ? __builtin_nontemporal_load(h.ucb + (long long)k * h.ld + j) : 0.0,
+                                  h.shift[k]);
           nan[u] = nan[u] || (p[u][k] != p[u][k]);
         }
       }
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
         const long long j = s0 + wave * wspan + 64 * u + lane;
         const bool in = j < a.n_cand;
         const double v = nan[u] ? __builtin_nan("") : hv[u];
-        if (in) h.acq_out[j] = v;
+        if (in) __builtin_nontemporal_store(v, h.acq_out + j);      // streamed: read by nothing here
         const bool ok = in && !xbit(a.xbits, j);
         dst.i[u] = ok ? a.cand_offset + j : -1;
         dst.k[u] = ok ? bo_order_key(v, 0) : 0ull;
@@ -837,7 +838,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long j = b_first + u * stride + lane;
-      pre[u] = j < a.n_cand ? a.acq[j] : 0.0;
+      pre[u] = j < a.n_cand ? __builtin_nontemporal_load(a.acq + j) : 0.0;
     }
   }
   if (a.lds_slots > 0) {
@@ -868,13 +869,13 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
       const bool in = j < a.n_cand;
       live[u] = in && !xbit(a.xbits, j);
       if constexpr (M == 0) {
-        val[u] = b0 == b_first ? pre[u] : (in ? a.acq[j] : 0.0);
+        val[u] = b0 == b_first ? pre[u] : (in ? __builtin_nontemporal_load(a.acq + j) : 0.0);
       } else {
         double p[M];
         bool nan = false;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
-          p[k] = __builtin_fma(h.scale[k], in ? h.ucb[(long long)k * h.ld + j] : 0.0, h.shift[k]);
+          p[k] = __builtin_fma(h.scale[k], in ? __builtin_nontemporal_load(h.ucb + (long long)k * h.ld + j) : 0.0, h.shift[k]);
           nan = nan || (p[k] != p[k]);
         }
         double hv = 0.0;
@@ -889,7 +890,7 @@ __global__ __launch_bounds__(256) void select_stream_kernel(SelArgs a, HviIn h) 
           hv += w;
         }
         val[u] = nan ? __builtin_nan("") : hv;
-        if (in) h.acq_out[j] = val[u];
+        if (in) __builtin_nontemporal_store(val[u], h.acq_out + j);
       }
       any = any || (live[u] && !(val[u] < tv));
     }

@@ -868,9 +868,43 @@ def main():
             res["front_hypervolume"] = {"value": hv_front, "reference_point": ref_pt.tolist(),
                                         "method": f"bo_box_volume_sum over this rank's share of the "
                                                   f"{n_boxes[0]} boxes + all_reduce(SUM) over {world} rank(s)"}
-            res["hvi_select"] = {"kernels": (f"select_small_kernel<{n_obj}, 4> + select_merge_kernel<4>" if q <= 4 else
+            # device time per call as select_standalone takes it: the step's masked call replayed
+            # as one HIP graph (no host launch gaps), after the timed region
+            hvi_graph_ms = None
+            if not args.hvi_unmasked:
+                boxes_g = torch.as_tensor(hypervolume_boxes(front_y, ref_pt), device=dev)
+
+                def hvi_call(strm):
+                    bo._lib.check(lib.bo_hvi_select_topq_masked(
+                        out["acq"].data_ptr(), out["ucb"].data_ptr(), per_rank, per_rank, n_obj, shift, scale,
+                        boxes_g.data_ptr(), boxes_g.shape[0], offset, hvi_mask.ptr, q, rec.data_ptr(),
+                        rec.data_ptr() + 8 * q, sel_ws.data_ptr(), sel_ws.numel(), strm), "hvi_select_masked")
+                side = torch.cuda.Stream(dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                gh = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(side):
+                    hvi_call(side.cuda_stream)
+                    with torch.cuda.graph(gh, stream=side):
+                        for _ in range(20):
+                            hvi_call(side.cuda_stream)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                gh.replay()
+                torch.cuda.synchronize()
+                g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                g0.record()
+                gh.replay()
+                g1.record()
+                torch.cuda.synchronize()
+                hvi_graph_ms = g0.elapsed_time(g1) / 20
+            in_step_ms = hms
+            if hvi_graph_ms is not None:
+                hms = hvi_graph_ms
+            res["hvi_select"] = {"kernels": (f"select_small_kernel<{n_obj}, 4> + select_rounds_merge_kernel" if q <= 4 else
                                              f"select_stream_kernel<{n_obj}, 4> + bo_topq_merge_kernel")
                                             + " (exact HVI + top-q, one pass)",
+                                 "timing": ("HIP-graph replay of the masked call, device time per call (as select_standalone)"
+                                            if hvi_graph_ms is not None else "event pair around the step's call"),
+                                 "in_step_event_ms": in_step_ms,
                                  "exclusion": ("per-call hash set of the points (bo_hvi_select_topq)" if args.hvi_unmasked
                                                else "persistent exclusion mask (bo_hvi_select_topq_masked)"),
                                  "excl_mask": None if args.hvi_unmasked else mask_ms,
@@ -978,7 +1012,7 @@ def standalone_select(lib, bo, acq, cands, offset, n, xd, q, dev, fused_sel, rep
 
     ms_p, ok_p = timed(call_points)
     ms, ok = timed(call_masked)
-    return {"kernels": ("select_small_kernel<0, 4> + select_merge_kernel<4>" if q <= 4 else
+    return {"kernels": ("select_small_kernel<0, 4> + select_rounds_merge_kernel" if q <= 4 else
                         "select_stream_kernel<0, 8> + bo_topq_merge_kernel") + " (HIP-graph replay)",
             "exclusion": "persistent exclusion mask (bo_select_topq_masked)",
             "ms": ms, "bytes": 8 * n, "achieved_GBps": 8 * n / (ms * 1e-3) / 1e9,

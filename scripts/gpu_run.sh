@@ -2,7 +2,7 @@
 # One GPU session of named steps, each under its own time limit; stops at the first step that
 # crashes, aborts or times out (pytest's rc 1 = test failures is reported and the run goes on).
 #   scripts/gpu_run.sh TAG step [step ...]
-#   steps: tests[:<pytest selection>]  smoke  bench[:<bench args>]  iter:<cfg>  fit:<cfg>
+#   steps: tests[:<files>[|<-k expr, + for space>]]  smoke  bench[:<bench args>]  iter:<cfg>  fit:<cfg>
 #          prof:<bench args>  (rocprofv3 --kernel-trace --stats of bench.py)
 #          py:<script args>  pyprof:<script args> (rocprofv3 of a python script)
 #          env:VAR=value (exported for the following steps; env:VAR= unsets it)
@@ -19,9 +19,16 @@ for st in "$@"; do
   kind=${st%%:*}; arg=""; [ "$kind" != "$st" ] && arg=${st#*:}
   case $kind in
     tests)
-      sel=${arg:-tests}
-      timeout -k 10 1200 python -u -m pytest $sel -m gpu -v --timeout 300 --timeout-method thread -rf \
-          > "$OUT/tests_$i.log" 2>&1; rc=$?
+      # tests:FILES or tests:FILES|KEXPR (a -k expression, '+' for a space: tests:x.py|a+or+b)
+      sel=${arg:-tests}; kx=""
+      if [ "${sel#*|}" != "$sel" ]; then kx=${sel#*|}; kx=${kx//+/ }; sel=${sel%%|*}; fi
+      if [ -n "$kx" ]; then
+        timeout -k 10 1200 python -u -m pytest $sel -k "$kx" -m gpu -v --timeout 300 --timeout-method thread -rf \
+            > "$OUT/tests_$i.log" 2>&1; rc=$?
+      else
+        timeout -k 10 1200 python -u -m pytest $sel -m gpu -v --timeout 300 --timeout-method thread -rf \
+            > "$OUT/tests_$i.log" 2>&1; rc=$?
+      fi
       echo "[$i] pytest $sel rc=$rc"; grep -E "passed|failed|error" "$OUT/tests_$i.log" | tail -3 ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
