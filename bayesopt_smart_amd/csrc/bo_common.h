@@ -447,6 +447,11 @@ int bo_lu_max_n();
 int bo_lu_inverse(double* const* out, const double* const* km, int n_lu, int64_t ld, int64_t n, double jitter,
                   void* ws, size_t ws_bytes, hipStream_t s);
 
+// the lean final merge of sorted top-q lists (bo_select.hip; q <= 4, n_lists <= 1024), used after
+// the fused kernel; false when it does not apply
+bool bo_launch_rounds_merge(const TopEntry* lists, long long n_lists, int q, double* out_v, int64_t* out_i,
+                            hipStream_t s);
+
 // ---------------------------------------------------------------------------------------
 // Sobol candidates (BO_CAND_SOBOL): direction numbers (host) and one coordinate (device).
 // ---------------------------------------------------------------------------------------

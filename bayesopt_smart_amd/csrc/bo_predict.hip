@@ -788,9 +788,13 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
   if (e != hipSuccess) return BO_ERR_HIP;
   if (timed) timer_mark(s);
   if (d->topq > 0) {
-    hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(256), 0, s, partial,
-                       (long long)pl.grid * pl.waves, d->topq, d->top_val, (long long*)d->top_idx);
-    BO_CHECK_HIP(hipGetLastError());
+    // q <= 4: the lean rounds merge (a lane per wave list, bo_select.hip); else the general one
+    const long long nl = (long long)pl.grid * pl.waves;
+    if (!bo_launch_rounds_merge(partial, nl, d->topq, d->top_val, d->top_idx, s)) {
+      hipLaunchKernelGGL(bo_topq_merge_kernel, dim3(1), dim3(256), 0, s, partial, nl, d->topq, d->top_val,
+                         (long long*)d->top_idx);
+      BO_CHECK_HIP(hipGetLastError());
+    }
   }
   return BO_OK;
 }

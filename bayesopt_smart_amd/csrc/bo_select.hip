@@ -762,19 +762,26 @@ __global__ __launch_bounds__(1024) void select_small_kernel(SelArgs a, HviIn h) 
 #endif
 }
 
-// Final merge of n_lists <= 1024 sorted top-q lists ([n_lists][q], q <= 4): one workgroup, a lane
-// per list, the lean rounds (block_topq_rounds) -- the lists hold no evaluated point.
+// Final merge of n_lists sorted top-q lists ([n_lists][q], q <= 4): one workgroup of up to 1024
+// threads, a lane per list (further lists folded in by the keep-best merge), the lean rounds
+// (block_topq_rounds) -- the lists hold no evaluated point.
 __global__ __launch_bounds__(1024) void select_rounds_merge_kernel(const TopEntry* __restrict__ L, int n_lists,
                                                                    int q, double* __restrict__ out_v,
                                                                    long long* __restrict__ out_i) {
   __shared__ TopEntry wl[16 * 4];
-  const int l = threadIdx.x, lane = l & 63;
+  const int lane = threadIdx.x & 63;
   LaneRun<4> run;
+  // a lane per list; more lists than threads fold in by the keep-best merge
+  for (int l = threadIdx.x; l < n_lists || l == (int)threadIdx.x; l += blockDim.x) {
+    LaneRun<4> nx;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const TopEntry e = (l < n_lists && u < q) ? L[(size_t)l * q + u] : TopEntry{-__builtin_inf(), -1};
-    run.i[u] = e.i;
-    run.k[u] = e.i >= 0 ? bo_order_key(e.v, 0) : 0ull;
+    for (int u = 0; u < 4; ++u) {
+      const TopEntry e = (l < n_lists && u < q) ? L[(size_t)l * q + u] : TopEntry{-__builtin_inf(), -1};
+      nx.i[u] = e.i;
+      nx.k[u] = e.i >= 0 ? bo_order_key(e.v, 0) : 0ull;
+    }
+    if (l == (int)threadIdx.x) run = nx;
+    else lane_keep_best<4>(run, nx);
   }
   double ov;
   long long oi;
@@ -1059,6 +1066,18 @@ int cus_count() {
 }
 
 }  // namespace
+
+// Internal (bo_predict.hip): the final merge of the fused kernel's per-wave lists by the lean
+// rounds when q <= 4 (returns false otherwise: the caller's general merge)
+bool bo_launch_rounds_merge(const TopEntry* lists, long long n_lists, int q, double* out_v, int64_t* out_i,
+                            hipStream_t s) {
+  if (q < 1 || q > 4 || n_lists < 1 || n_lists > (1LL << 30)) return false;
+  const long long t = n_lists < 1024 ? n_lists : 1024;
+  const unsigned threads = (unsigned)((t + 63) / 64 * 64);
+  hipLaunchKernelGGL(select_rounds_merge_kernel, dim3(1), dim3(threads), 0, s, lists, (int)n_lists, q, out_v,
+                     (long long*)out_i);
+  return hipGetLastError() == hipSuccess;
+}
 
 extern "C" {
 
