@@ -554,141 +554,12 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
     }
   }
   if (blockIdx.x == 0) {
-    bool singular = false;
-    if constexpr (LR == 1) {
-    // factor strip k: columns j, pivot rows g0 = 16 k + j.  A ROLLED loop (the unrolled one was
-    // ~60 KB of code run once per launch: instruction fetch, not arithmetic, set its 36 us).
-    // Column j is read and written through its wave-uniform index (s_set_gpr_idx, no scratch);
-    // the update covers the statically indexed columns c > j.  (Round 4 rotated the rows so that
-    // column j sat at index 0: 16 moves per row and column.)  The swap writes run only in the
-    // waves that hold row g0 or the pivot row (a ballot makes the test wave-uniform).
-#pragma unroll 1
-    for (int j = 0; j < LB; ++j) {
-      const int bf = j & 1;
-      const long long g0 = (long long)LB * k + j;
-      LU_CSTAMP(k, j, 0);
-      unsigned long long bk = 0ull;
-      int brow = 0x7fffffff;
-      double cj[LR], rcp[LR];
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        cj[r] = w[r][j];
-        // every row's reciprocal (getf2 scales by 1 / pivot), issued before the wave reduction so
-        // that the division's latency overlaps it instead of following it
-        rcp[r] = 1.0 / cj[r];
-      }
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const long long row = own_row(base, r);
-        const unsigned long long kr = piv_key(cj[r], row >= g0 && row < g.n_p);
-        if (kr > bk) { bk = kr; brow = (int)row; }                   // first max per thread
-      }
-      unsigned long long wk;
-      int wrow;
-      piv_wave_best(bk, brow, wk, wrow);
-      LU_CSTAMP(k, j, 1);
-      // the wave's pivot candidate row and its reciprocal
-#pragma unroll
-      for (int r = 0; r < LR; ++r)
-        if (wk != 0ull && own_row(base, r) == wrow) {
-#pragma unroll
-          for (int c = 0; c < LB; c += 2) *(d2*)&L.cand[bf][wave][c] = (d2){w[r][c], w[r][c + 1]};
-          L.crp[bf][wave] = rcp[r];
-        }
-      if (lane == 0) {
-        L.ck[bf][wave] = wk;
-        L.cr[bf][wave] = wk != 0ull ? wrow : 0x7fffffff;
-      }
-#pragma unroll
-      for (int r = 0; r < LR; ++r)
-        if (own_row(base, r) == g0) {
-#pragma unroll
-          for (int c = 0; c < LB; c += 2) *(d2*)&L.grow[bf][c] = (d2){w[r][c], w[r][c + 1]};
-          L.grp[bf] = rcp[r];
-        }
-      __syncthreads();
-      LU_CSTAMP(k, j, 2);
-      unsigned long long kk[LW];
-      int rr[LW], ww[LW];
-#pragma unroll
-      for (int u = 0; u < LW; ++u) { kk[u] = L.ck[bf][u]; rr[u] = L.cr[bf][u]; ww[u] = u; }
-      // the workgroup's pivot: a 3-level tree over the 8 wave candidates (depth 3, not 7)
-#pragma unroll
-      for (int h = LW / 2; h >= 1; h >>= 1)
-#pragma unroll
-        for (int u = 0; u < h; ++u) {
-          const bool t = piv_before(kk[u + h], rr[u + h], kk[u], rr[u]);
-          kk[u] = t ? kk[u + h] : kk[u];
-          rr[u] = t ? rr[u + h] : rr[u];
-          ww[u] = t ? ww[u + h] : ww[u];
-        }
-      const unsigned long long pk = kk[0];
-      int p = rr[0], pw = ww[0];
-      // pk - 1 = bits of |pivot|: a zero (or NaN-only) column is singular
-      const bool zero = pk <= 1ull;
-      if (zero) { singular = true; p = (int)g0; pw = -1; }           // zero / NaN column: no swap
-      const double* prow = pw >= 0 ? L.cand[bf][pw] : L.grow[bf];
-      if (tid == 0) L.piv[j] = p;
-      // the pivot row in registers first: every LDS read in flight at once
-      double pr[LB];
-#pragma unroll
-      for (int c = 0; c < LB; c += 2) {
-        const d2 v = *(const d2*)(prow + c);
-        pr[c] = v.x;
-        pr[c + 1] = v.y;
-      }
-      const double rp = pw >= 0 ? L.crp[bf][pw] : L.grp[bf];
-      // the swap: row g0 takes the pivot row, row p takes row g0 (only the waves holding them)
-      bool hg[LR], hp[LR], any = false;
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const long long row = own_row(base, r);
-        hg[r] = row == g0;
-        hp[r] = !hg[r] && row == p;
-        any = any || hg[r] || hp[r];
-      }
-      if (__ballot(any) != 0ull) {                                   // wave-uniform
-#pragma unroll
-        for (int r = 0; r < LR; ++r) {
-          if (hg[r]) {
-#pragma unroll
-            for (int c = 0; c < LB; ++c) w[r][c] = pr[c];
-          } else if (hp[r]) {
-#pragma unroll
-            for (int c = 0; c < LB; c += 2) {
-              const d2 v = *(const d2*)&L.grow[bf][c];
-              w[r][c] = v.x;
-              w[r][c + 1] = v.y;
-            }
-          }
-        }
-      }
-      double l[LR];
-      bool act[LR];
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const long long row = own_row(base, r);
-        act[r] = row > g0 && row < g.n_p;
-        l[r] = w[r][j] * rp;
-        if (act[r]) w[r][j] = l[r];
-      }
-#pragma unroll
-      for (int c = 1; c < LB; ++c)
-        if (c > j) {                                                 // uniform
-#pragma unroll
-          for (int r = 0; r < LR; ++r)
-            if (act[r]) w[r][c] = __builtin_fma(-l[r], pr[c], w[r][c]);
-        }
-      LU_CSTAMP(k, j, 3);
-    }
-    } else {
-    // LR >= 2: the rows rotate so that column j sits at index 0 (a uniform index into the
-    // two-dimensional row array spills: 272-528 B of scratch per lane)
     // factor strip k: columns j, pivot rows g0 = 16 k + j.  A ROLLED loop (the unrolled one was
     // ~60 KB of code run once per launch: instruction fetch, not arithmetic, set its 36 us), so
     // the rows rotate instead of being indexed by j: at column j, w[r][0] is column j, w[r][c] is
     // column j + c for c < 16 - j, and w[r][16 - j + i] is the finished column i.  Sixteen
     // rotations restore the natural order.
+    bool singular = false;
 #pragma unroll 1
     for (int j = 0; j < LB; ++j) {
       const int bf = j & 1;
@@ -799,7 +670,6 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
         w[r][LB - 1] = t;
       }
       LU_CSTAMP(k, j, 3);
-    }
     }
     if (tid == 0 && singular) bt.status[slot] = 1;
     __syncthreads();                                  // L.piv complete
