@@ -29,8 +29,14 @@ for r in rows:
     base = next(x for x in rows if x["config"]["workload"] == c["workload"] and x["n_gpus"] == 1)
     same = r["selected"] == base["selected"]
     ok &= same
+    ro = r.get("roofline", {})
+    ss = r.get("select_standalone") or {}
+    local_ok = ss.get("matches_fused_selection")
+    ok &= local_ok is not False
     print(c["workload"][:3], "P =", r["n_gpus"], "per rank", c["n_cand_per_gpu"], "offset(rank 0)", c["candidate_offset"],
-          "selected", r["selected"], "same as P=1:", same)
+          "selected", r["selected"], "same as P=1:", same, "| traffic", ro.get("traffic"), "ratio",
+          ro.get("traffic_ratio"), "| select_standalone vs the rank-local fused selection:", local_ok,
+          "| collectives", r.get("collectives"))
 print("all equal:", ok)
 sys.exit(0 if ok else 1)
 EOF
