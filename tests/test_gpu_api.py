@@ -282,6 +282,31 @@ def test_orchestrator_exact_hvi_acquisition(bo):
     np.testing.assert_array_equal(seen[0], O.select_next_batch(grid, ref, x, 3))
 
 
+def test_orchestrator_exact_hvi_loop_extends_the_exclusion_mask(bo):
+    """The exact-HVI loop keeps one exclusion mask per shard (acquisition.ExclusionMask) and
+    extends it by each iteration's batch: over 4 iterations every batch equals the oracle's
+    select_next_batch (acquisition.py:116-144) over that iteration's acquisition array with the
+    points evaluated before it excluded."""
+    from bayesopt_smart_amd.bayesian_optimization import BayesianOptimization
+
+    def toy(x):
+        return np.array([-((x[0] - 60) ** 2) + 100, -((x[1] - 50) ** 2) + 20], dtype=np.float64)
+
+    states = []
+    np.random.seed(7)
+    opt = BayesianOptimization(toy, [(0, 120), (0, 120)], n_objectives=2, initial_samples=6,
+                               n_iterations=4, batch_size=3, betas=np.array([2.0, 2.0]),
+                               acquisition="hvi", reference_point=[-3e4, -3e4],
+                               callbacks=[lambda s: states.append((s["iteration"], np.array(s["x_vector"]),
+                                                                   np.array(s["acquisition_values"]),
+                                                                   np.array(s["x_next"])))])
+    opt.optimize()
+    grid = O.grid_points([(0, 120), (0, 120)])
+    assert len(states) == 4
+    for it, xv, acq, xn in states:
+        np.testing.assert_array_equal(xn, O.select_next_batch(grid, acq, xv[:it], 3))
+
+
 @pytest.mark.parametrize("it", [6, 9, 12])
 def test_demo_trajectory_replay_each_iteration(bo, it):
     """Every recorded iteration of the reference's headless demo run (G6), replayed on the

@@ -2,7 +2,8 @@
 put_perm/apply_perm): a step's 16 row swaps (rows 16 s + j <-> piv[j], in order, as LAPACK's
 laswp applies getrf's ipiv) composed by wave 0 into <= 32 (pos <- src) pairs -- lane u holds slot
 u: its row and the row whose data ends there; a row not yet in a slot is appended at slot m --
-then applied through the row -> slot maps.  The model follows the kernel's slot algorithm and
+then applied through the row -> slot maps.  The model follows round 4's slot algorithm and the
+kernel's data-parallel one (round 5: each lane follows its row's data) and
 compares it with the swaps applied one by one.  Test infrastructure only; no GPU."""
 import numpy as np
 import pytest
@@ -28,6 +29,25 @@ def build_perm(s, piv):
         srcs[ia], srcs[ib] = srcs[ib], srcs[ia]
     assert len(rows) <= 32                       # the record holds 32 slots
     return [(r, c) for r, c in zip(rows, srcs) if r != c]
+
+
+def build_perm_parallel(s, piv):
+    """build_perm as the kernel computes it since round 5: lane j < 16 takes row 16 s + j, lane
+    16 + j row piv[j]; a row named twice keeps its first lane; each lane follows its row's data
+    through the swaps to its final position v; the pairs (pos = v, src = row) of the moved rows,
+    compacted in lane order."""
+    rows = [LB * s + j for j in range(LB)] + [int(p) for p in piv]
+    out = []
+    for lane, r0 in enumerate(rows):
+        if r0 in rows[:lane]:
+            continue
+        v = r0
+        for j in range(LB):
+            a, b = LB * s + j, int(piv[j])
+            v = b if v == a else (a if v == b else v)
+        if v != r0:
+            out.append((v, r0))
+    return out
 
 
 def apply_record(x, rec):
@@ -67,7 +87,8 @@ def test_perm_record_equals_sequential_swaps(seed):
         lo = LB * s
         piv = [int(v) for v in rng.permutation(np.arange(lo + LB, n))[:LB]]
     x = rng.standard_normal((n, 3))
-    rec = build_perm(s, piv)
-    np.testing.assert_array_equal(apply_record(x, rec), apply_swaps(x, s, piv))
-    poss = [p for p, _ in rec]
-    assert len(set(poss)) == len(poss) and sorted(poss) == sorted(c for _, c in rec)
+    for rec in (build_perm(s, piv), build_perm_parallel(s, piv)):
+        np.testing.assert_array_equal(apply_record(x, rec), apply_swaps(x, s, piv))
+        poss = [p for p, _ in rec]
+        assert len(set(poss)) == len(poss) and sorted(poss) == sorted(c for _, c in rec)
+    assert sorted(build_perm(s, piv)) == sorted(build_perm_parallel(s, piv))
