@@ -645,23 +645,34 @@ __device__ __forceinline__ void mfma_fence_acc(d4 (&acc)[2][2]) {
 //   MODE 1:  out = X + X R                     (A operand: X)
 // Both A operands are symmetric (the Cholesky path runs only for a symmetric K; X is the
 // mirrored lower triangle), so A[i][k] is read as A[k][i]: every operand load is 16 consecutive
-// doubles of a row.  64 x 64 output tile per workgroup, 32 x 32 per wave (2 x 2
-// v_mfma_f64_16x16x4_f64 blocks), k in blocks of 32 with the next block's loads in flight.
-template <int MODE>
+// doubles of a row.  32 x 32 per wave (2 x 2 v_mfma_f64_16x16x4_f64 blocks), k in blocks of 32
+// with the next block's loads in flight.
+//   SPLITK (n <= 1024): a 32 x 32 tile per workgroup, k split over its 4 waves (a quarter of n
+//     each), the partial tiles summed through LDS in a fixed order (deterministic): 4x the waves
+//     of the other form at N = 512, where it was latency-bound (update_k + invert_k 0.272 ->
+//     0.241 ms at C3);
+//   otherwise a 64 x 64 tile per workgroup, each wave its own 32 x 32 tile over the whole k (at
+//     N = 2048 the split form measured 4.29 vs 4.14 ms).
+template <int MODE, bool SPLITK>
 __global__ __launch_bounds__(256) void inv_refine_kernel(const double* __restrict__ Am, long long lda, long long a_os,
                                                          double jitter, const double* __restrict__ Bm,
                                                          long long b_os, const double* __restrict__ Xm,
                                                          long long x_os, double* __restrict__ D, long long d_os,
                                                          int n, const int* __restrict__ status) {
+  __shared__ double part[SPLITK ? 3 : 1][32][33];
   const int o = blockIdx.z;
   if (status[o]) return;                        // LU objective: refined by nothing (gesv itself)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, lg = lane >> 4;
-  const int i0 = blockIdx.y * 64 + (wave >> 1) * 32, j0 = blockIdx.x * 64 + (wave & 1) * 32;
-  if (i0 >= n || j0 >= n) return;               // wave-uniform; no barriers below
+  const int i0 = SPLITK ? blockIdx.y * 32 : blockIdx.y * 64 + (wave >> 1) * 32;
+  const int j0 = SPLITK ? blockIdx.x * 32 : blockIdx.x * 64 + (wave & 1) * 32;
+  if (!SPLITK && (i0 >= n || j0 >= n)) return;   // wave-uniform; no barriers below
   const double* Ao = Am + (long long)o * a_os;
   const double* Bo = Bm + (long long)o * b_os;
   const long long ldb = n;
+  // this wave's k range: a quarter of n, rounded to whole k-steps of 4 (SPLITK), else all of it
+  const int kq = ((n + 15) / 16) * 4;
+  const int k_lo = SPLITK ? wave * kq : 0, k_hi = SPLITK ? min(n, (wave + 1) * kq) : n;
   bool ca[2], cb[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -674,7 +685,7 @@ __global__ __launch_bounds__(256) void inv_refine_kernel(const double* __restric
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k = kb + 4 * s + lg;
-      const bool kok = k < n;
+      const bool kok = k < k_hi;
       const double* ra = Ao + (long long)k * lda;
       const double* rb = Bo + (long long)k * ldb;
 #pragma unroll
@@ -701,15 +712,30 @@ __global__ __launch_bounds__(256) void inv_refine_kernel(const double* __restric
         for (int b = 0; b < 2; ++b) acc[a][b] = mfma64(av[buf][s][a], bv[buf][s][b], acc[a][b]);
   };
   // ping-pong with static buffer indices (a variable index puts the arrays in scratch)
-  load(0, 0);
-  for (int kb = 0; kb < n; kb += 8 * KS) {
-    if (kb + 4 * KS < n) load(1, kb + 4 * KS);
-    compute(0);
-    if (kb + 4 * KS >= n) break;
-    if (kb + 8 * KS < n) load(0, kb + 8 * KS);
-    compute(1);
+  if (k_lo < k_hi) {                            // wave-uniform
+    load(0, k_lo);
+    for (int kb = k_lo; kb < k_hi; kb += 8 * KS) {
+      if (kb + 4 * KS < k_hi) load(1, kb + 4 * KS);
+      compute(0);
+      if (kb + 4 * KS >= k_hi) break;
+      if (kb + 8 * KS < k_hi) load(0, kb + 8 * KS);
+      compute(1);
+    }
   }
   mfma_fence_acc(acc);
+  // waves 1..3 hand their partial tiles to wave 0 (D layout: row 16 a + lg + 4 r, column 16 b + li)
+  if (SPLITK && wave > 0) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[wave - 1][16 * a + lg + 4 * r][16 * b + li] = acc[a][b][r];
+  }
+  if constexpr (SPLITK) {
+    __syncthreads();
+    if (wave != 0) return;
+  }
   const double* Xo = Xm + (long long)o * x_os;
   double* Do = D + (long long)o * d_os;
 #pragma unroll
@@ -718,10 +744,13 @@ __global__ __launch_bounds__(256) void inv_refine_kernel(const double* __restric
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = i0 + 16 * a + lg + 4 * r, j = j0 + 16 * b + li;
+        const int ti = 16 * a + lg + 4 * r, tj = 16 * b + li;
+        const int i = i0 + ti, j = j0 + tj;
         if (i >= n || j >= n) continue;
+        const double v = SPLITK ? ((acc[a][b][r] + part[0][ti][tj]) + part[1][ti][tj]) + part[SPLITK ? 2 : 0][ti][tj]
+                                : acc[a][b][r];
         const long long e = (long long)i * n + j;
-        Do[e] = MODE == 0 ? ((i == j ? 1.0 : 0.0) - acc[a][b][r]) : Xo[e] + acc[a][b][r];
+        Do[e] = MODE == 0 ? ((i == j ? 1.0 : 0.0) - v) : Xo[e] + v;
       }
 }
 
@@ -1545,12 +1574,14 @@ int inv_finish(double* out, double* A, const Geo& g, const double* km, long long
   double* X = A;                               // objective o: X at A_o, R at A_o + n^2 (< 2 n_p^2)
   double* R = A + n * n;
   hipLaunchKernelGGL(inv_extract_kernel, dim3(nt, nt, g.n_obj), dim3(256), 0, s, X, g.ostride, A, g, status);
-  const unsigned t64 = (unsigned)((n + 63) / 64);
-  hipLaunchKernelGGL(inv_refine_kernel<0>, dim3(t64, t64, g.n_obj), dim3(256), 0, s, km, ld, ld * ld, jitter,
-                     (const double*)X, g.ostride, (const double*)nullptr, 0ll, R, g.ostride, (int)n, status);
-  hipLaunchKernelGGL(inv_refine_kernel<1>, dim3(t64, t64, g.n_obj), dim3(256), 0, s, (const double*)X, n,
-                     g.ostride, 0.0, (const double*)R, g.ostride, (const double*)X, g.ostride, out, n * n, (int)n,
-                     status);
+  const bool split = n <= 1024;
+  const unsigned tt = (unsigned)(split ? (n + 31) / 32 : (n + 63) / 64);
+  auto k0 = split ? inv_refine_kernel<0, true> : inv_refine_kernel<0, false>;
+  auto k1 = split ? inv_refine_kernel<1, true> : inv_refine_kernel<1, false>;
+  hipLaunchKernelGGL(k0, dim3(tt, tt, g.n_obj), dim3(256), 0, s, km, ld, ld * ld, jitter, (const double*)X, g.ostride,
+                     (const double*)nullptr, 0ll, R, g.ostride, (int)n, status);
+  hipLaunchKernelGGL(k1, dim3(tt, tt, g.n_obj), dim3(256), 0, s, (const double*)X, n, g.ostride, 0.0,
+                     (const double*)R, g.ostride, (const double*)X, g.ostride, out, n * n, (int)n, status);
   return hipGetLastError() == hipSuccess ? BO_OK : BO_ERR_HIP;
 }
 
