@@ -352,6 +352,7 @@ struct PrepArgs {
   int* hidx;
   unsigned int hslots;
   int n_hash;                            // rows to insert (0: no table)
+  int hash_lds;                          // 1: built in the launch's dynamic LDS, then stored
 };
 
 __global__ __launch_bounds__(256) void predict_prep_kernel(const PrepArgs p) {
@@ -398,16 +399,28 @@ __global__ __launch_bounds__(256) void predict_prep_kernel(const PrepArgs p) {
         kp[u] = bo_point_key(c, p.DIM);
       }
     }
-    for (unsigned int t = tid; t < p.hslots; t += 256) p.hkeys[t] = 0ull;
+    // small tables (hash_lds) are built in LDS -- LDS compare-and-swaps instead of a chain of
+    // global atomic round trips -- and then stored with plain coalesced stores
+    extern __shared__ unsigned long long hls[];
+    unsigned long long* keys = p.hash_lds ? hls : p.hkeys;
+    int* idx = p.hash_lds ? (int*)(hls + p.hslots) : p.hidx;
+    for (unsigned int t = tid; t < p.hslots; t += 256) keys[t] = 0ull;
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < KP; ++u)
-      if (kp[u] != 0ull) bo_hash_insert(p.hkeys, p.hidx, p.hslots - 1, kp[u], tid + 256 * u);
+      if (kp[u] != 0ull) bo_hash_insert(keys, idx, p.hslots - 1, kp[u], tid + 256 * u);
     for (int e = tid + 256 * KP; e < p.n_hash; e += 256) {
       double c[BO_MAX_DIM];
       for (int k = 0; k < p.DIM; ++k) c[k] = k < p.dim ? src[(long long)e * p.dim + k] : 0.0;
       const unsigned long long key = bo_point_key(c, p.DIM);
-      if (key != 0ull) bo_hash_insert(p.hkeys, p.hidx, p.hslots - 1, key, e);
+      if (key != 0ull) bo_hash_insert(keys, idx, p.hslots - 1, key, e);
+    }
+    if (p.hash_lds) {
+      __syncthreads();
+      for (unsigned int t = tid; t < p.hslots; t += 256) {
+        p.hkeys[t] = keys[t];
+        p.hidx[t] = idx[t];
+      }
     }
     return;
   }
@@ -759,8 +772,10 @@ static int predict_impl(const bo_predict_desc* d, const double* kstar, long long
     pa.hidx = (int*)fa.hidx;
     pa.hslots = pl.hash_slots;
     pa.n_hash = (kmem || d->topq == 0) ? 0 : pl.n_excl;
+    pa.hash_lds = pa.n_hash > 0 && pl.hash_slots <= 2048 ? 1 : 0;     // <= 24 KiB of LDS
+    const size_t prep_lds = pa.hash_lds ? (size_t)pl.hash_slots * 12 : 0;
     hipLaunchKernelGGL(predict_prep_kernel, dim3((unsigned)(2 + pa.alpha_blocks + pa.pack_blocks)), dim3(256),
-                       0, s, pa);
+                       prep_lds, s, pa);
     BO_CHECK_HIP(hipGetLastError());
   }
   if (d->n_cand == 0) {
