@@ -50,10 +50,8 @@ def exchange_topq_rec(rec, q, group=None, out=None):
         out = None
     g = out if out is not None else torch.empty(world * 2 * q, dtype=rec.dtype, device=rec.device)
     dist.all_gather_into_tensor(g, rec.contiguous(), group=group)
-    g = g.view(world, 2 * q)
-    vals = g[:, :q].cpu().numpy()
-    idxs = g[:, q:].contiguous().view(torch.int64).cpu().numpy()
-    return merge_topq(vals, idxs, q)
+    gh = g.cpu().numpy().reshape(world, 2 * q)      # one device-to-host copy of the whole block
+    return merge_topq(gh[:, :q], gh[:, q:].view(np.int64), q)
 
 
 def exchange_topq(top_val, top_idx, q, group=None):

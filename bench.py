@@ -663,6 +663,10 @@ def main():
         else torch.empty(2 * q, dtype=torch.float64).pin_memory()
     rec_np = rec.numpy() if rec.device.type == "cpu" else None
     gath = torch.empty(world * 2 * q, dtype=torch.float64, device=dev)
+    # the gathered records land in a preallocated pinned buffer (one async copy + a stream
+    # synchronisation per step instead of a pageable allocation and copy)
+    gath_h = torch.empty(world * 2 * q, dtype=torch.float64).pin_memory()
+    gath_np = gath_h.numpy().reshape(world, 2 * q)
 
     hvi_ev = []
     if args.acq == "hvi":
@@ -743,12 +747,11 @@ def main():
         if use_dist:
             if backend == "nccl":
                 dist.all_gather_into_tensor(gath, rec)
-                g = gath.view(world, 2 * q).cpu()
+                gath_h.copy_(gath, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
             else:
-                g = torch.empty(world * 2 * q, dtype=torch.float64)
-                dist.all_gather_into_tensor(g, rec.cpu())
-                g = g.view(world, 2 * q)
-            return bo.merge_topq(g[:, :q].numpy(), g[:, q:].contiguous().view(torch.int64).numpy(), q)
+                dist.all_gather_into_tensor(gath_h, rec.cpu())
+            return bo.merge_topq(gath_np[:, :q], gath_np[:, q:].view(np.int64), q)
         # one shard: the device list is already merged and in selection order
         if rec_np is not None:
             torch.cuda.current_stream(dev).synchronize()
