@@ -820,7 +820,9 @@ def main():
         # the PMC summary key: the config in its default precision, "-<mode>" otherwise
         pmc_key = args.config if args.mode == ("fp32" if args.config == "C5" else "auto") \
             else f"{args.config}-{args.mode}"
-        traffic, traffic_src = pmc_traffic(pmc_key) if args.acq == "sum_ucb" else (None, None)
+        traffic, traffic_src = pmc_traffic(pmc_key) if args.acq == "sum_ucb" else \
+            (None, "not measured: the committed PMC passes run the sum-of-UCB step (this step writes "
+                   "the per-objective UCB the exact HVI reads)")
         if world > 1 and traffic is not None:
             # the committed PMC summaries are single-GPU runs over the whole candidate set: not
             # this rank's per-launch traffic

@@ -120,6 +120,51 @@ def test_masked_select_equals_unmasked_and_numpy(bo, q, kind):
     np.testing.assert_array_equal(got, ref)
 
 
+@pytest.mark.parametrize("q", [3, 16])
+def test_masked_select_on_a_shard(bo, q):
+    """A rank's shard [offset, offset + count): the mask covers the shard (local bit j = global
+    candidate offset + j) and the masked selection returns global indices, equal to the
+    per-call exclusion over the same shard and to numpy's order on it."""
+    import ctypes
+    import torch
+    from bayesopt_smart_amd import _lib
+    from bayesopt_smart_amd.acquisition import ExclusionMask, _grid_args
+    cands = bo.predict.CandidateSet.grid([(0, 1024), (0, 1024)])
+    offset, count = 3 * (1 << 18) + 77, (1 << 18) - 300          # shard 3 of 4, ragged
+    rng = np.random.default_rng(q + 100)
+    acq = rng.standard_normal(count)
+    hot_local = rng.choice(count, 200, replace=False)
+    acq[hot_local[:40]] = 30.0 + np.arange(40)                 # the shard's top: evaluated
+    out_of_shard = rng.choice(offset, 100, replace=False)      # evaluated points elsewhere
+    ev = cands.points(np.concatenate([offset + hot_local, out_of_shard])).astype(np.float64)
+    m = ExclusionMask(cands, offset, count, "cuda").update(ev)
+    lib = _lib.load()
+    acq_d = torch.tensor(acq, device="cuda")
+    ws = torch.empty(lib.bo_select_topq_workspace_size(count, q), dtype=torch.uint8, device="cuda")
+    res = {}
+    for masked in (True, False):
+        tv = torch.empty(q, dtype=torch.float64, device="cuda")
+        ti = torch.empty(q, dtype=torch.int64, device="cuda")
+        if masked:
+            st = lib.bo_select_topq_masked(acq_d.data_ptr(), count, offset, m.ptr, q, tv.data_ptr(), ti.data_ptr(),
+                                           ws.data_ptr(), ws.numel(), None)
+        else:
+            ex = torch.tensor(ev, device="cuda")
+            lo, sh = _grid_args(cands)
+            st = lib.bo_select_topq(acq_d.data_ptr(), count, cands.kind_code, None, lo, sh, 2, offset,
+                                    ex.data_ptr(), ex.shape[0], q, tv.data_ptr(), ti.data_ptr(), ws.data_ptr(),
+                                    ws.numel(), None)
+        _lib.check(st, "select")
+        torch.cuda.synchronize()
+        res[masked] = ti.cpu().numpy()
+    excl = np.zeros(count, dtype=bool)
+    excl[hot_local] = True
+    order = np.lexsort((np.arange(count), -np.where(excl, -np.inf, acq)))
+    np.testing.assert_array_equal(res[True], offset + order[:q])
+    np.testing.assert_array_equal(res[True], res[False])
+    del ctypes
+
+
 def test_masked_select_everything_excluded(bo):
     """A shard whose candidates are all evaluated yields an empty batch (index -1 entries)."""
     import torch
