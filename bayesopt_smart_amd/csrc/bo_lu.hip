@@ -69,13 +69,22 @@ __device__ int bo_lu_tcount;
       }                                                                              \
     }                                                                                \
   } while (0)
-// per pivot column of the panel (slot 0, steps < 64): plain stores of the clock, no atomics
+// per pivot column of the panel (slot 0, steps < 64; BO_LU_COLSTAMP builds only -- the stores
+// are waited for at every barrier, which inflates the phases they time): plain stores of the
+// clock, no atomics, and the shader clock beside it (their ratio is the core clock)
 __device__ long long bo_lu_cstamp[64 * LB_DIAG * 4];
+__device__ long long bo_lu_cclk[64 * LB_DIAG * 4];
+#ifdef BO_LU_COLSTAMP
 #define LU_CSTAMP(step, j, t)                                                        \
   do {                                                                               \
-    if (threadIdx.x == 0 && blockIdx.y == 0 && (step) < 64)                          \
+    if (threadIdx.x == 0 && blockIdx.y == 0 && (step) < 64) {                        \
       bo_lu_cstamp[((step) * LB_DIAG + (j)) * 4 + (t)] = (long long)wall_clock64();  \
+      bo_lu_cclk[((step) * LB_DIAG + (j)) * 4 + (t)] = (long long)clock64();         \
+    }                                                                                \
   } while (0)
+#else
+#define LU_CSTAMP(step, j, t) ((void)0)
+#endif
 #else
 #define LU_STAMP(step, tag) ((void)0)
 #define LU_CSTAMP(step, j, t) ((void)0)
@@ -84,12 +93,10 @@ __device__ long long bo_lu_cstamp[64 * LB_DIAG * 4];
 struct LuGeo {
   int n, n_p, nbs;              // N, N padded to 16, strips
   long long Na;                 // leading dimension (= n_p)
-  int small_panel;              // 1: factor a strip of <= SP_ROWS rows on SPW waves (panel_small)
+  int small_panel;              // 0 never, 1 above N_p = 512, 2 always: the 4-wave panel (panel_small)
 };
 
-constexpr int SPW = 2;                  // waves of the small panel
-constexpr int SPR = 4;                  // its rows per lane
-constexpr int SP_ROWS = SPW * 64 * SPR; // 512
+constexpr int SPW = 4;                  // waves of the small panel (one per SIMD)
 
 struct LuBatch {                // one factorisation per slot (the objectives whose Cholesky failed)
   double* A[BO_MAX_OBJ];
@@ -131,11 +138,10 @@ struct StripLds {
   double T[LB][LB + 1];         // the 16 x 16 block being solved
   double L11[LB][LB + 1];       // the step's diagonal block (L unit lower / U upper)
   alignas(16) double cand[2][LW][LB];   // panel: each wave's best row, by column parity
-  unsigned long long ck[2][LW]; //        its pivot key
+  unsigned long long ck[2][LW]; //        its pivot key (piv_key; 0: no candidate row)
   int cr[2][LW];                //        its row index
   double crp[2][LW];            //        1 / its entry in the column (the pivot's reciprocal)
   alignas(16) double grow[2][LB];       //        row j of the column
-  double grp[2];                //        1 / its entry
   int piv[LB];                  //        the step's pivot rows
   short smap[LT * LRMAX];          // row -> its slot as a source of the permutation (-1: none)
   short pmap[LT * LRMAX];          // row -> its slot as a destination
@@ -191,44 +197,6 @@ __device__ __forceinline__ void apply_perm(StripLds& L, double (&w)[LR][LB], int
   }
   __syncthreads();
   if ((int)threadIdx.x < m) { L.smap[L.src[threadIdx.x]] = -1; L.pmap[L.pos[threadIdx.x]] = -1; }
-}
-
-// Pivot search key of an entry: 0 for a row outside the column (or NaN: idamax skips it),
-// else the bits of |a| + 1 (monotone in |a| for non-negative doubles).  Ties go to the lower row.
-__device__ __forceinline__ unsigned long long piv_key(double a, bool in) {
-  const double v = fabs(a);
-  return (in && v == v) ? (unsigned long long)__double_as_longlong(v) + 1ull : 0ull;
-}
-__device__ __forceinline__ bool piv_before(unsigned long long ka, int ra, unsigned long long kb, int rb) {
-  return ka > kb || (ka == kb && ra < rb);
-}
-template <int CTRL>
-__device__ __forceinline__ void piv_dpp_step(unsigned long long& k, int& r) {
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)k, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(k >> 32), CTRL, 0xF, 0xF, false);
-  const int orr = __builtin_amdgcn_update_dpp(0, r, CTRL, 0xF, 0xF, false);
-  const unsigned long long ok = ((unsigned long long)(unsigned int)hi << 32) | (unsigned int)lo;
-  const bool t = piv_before(ok, orr, k, r);
-  k = t ? ok : k;
-  r = t ? orr : r;
-}
-// the wave's best (key, row), wave-uniform: quad_perm xor 1 and xor 2, row_half_mirror,
-// row_mirror (each 16-lane row then holds its best), then the 4 row bests by v_readlane
-__device__ __forceinline__ void piv_wave_best(unsigned long long k, int r, unsigned long long& wk, int& wr) {
-  piv_dpp_step<0xB1>(k, r);
-  piv_dpp_step<0x4E>(k, r);
-  piv_dpp_step<0x141>(k, r);
-  piv_dpp_step<0x140>(k, r);
-  wk = bo_readlane_u(k, 0);
-  wr = __builtin_amdgcn_readlane(r, 0);
-#pragma unroll
-  for (int l = 16; l < 64; l += 16) {
-    const unsigned long long rk = bo_readlane_u(k, l);
-    const int rr = __builtin_amdgcn_readlane(r, l);
-    const bool t = piv_before(rk, rr, wk, wr);
-    wk = t ? rk : wk;
-    wr = t ? rr : wr;
-  }
 }
 
 // Wave 0: the 16 swaps (rows 16 s + j <-> piv[j], in order) composed into pos <- src pairs over
@@ -378,80 +346,148 @@ __device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const 
   __syncthreads();                                   // L.T is rewritten by the next phase
 }
 
-// The panel of strip k when its rows to factor (16 k .. n_p) number at most SP_ROWS: they move
-// through LDS (P, column-major) from the workgroup's 8 waves to SPW = 2 waves, SPR = 4 rows per
-// lane in registers (row offset o = 256 wave + 64 r + lane), the other waves end, and each pivot
-// column synchronises two waves instead of eight.  The arithmetic is the 8-wave loop's, operation
-// for operation (the same pivot order, reciprocal and FMAs: bit-identical factors); the rows of
-// step k-1's U block (base .. 16 k) are stored by their threads before the hand-off.
-template <int LR>
-__device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, double* __restrict__ P,
-                            const double (&w)[LR][LB], int base, long long c0, double* __restrict__ A,
-                            int* __restrict__ prec, int slot) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int top = LB * k, R = g.n_p - top;
+// ------------------------------------------------------------- the pivot columns of a panel
+// Pivot search key of an entry: 0 for a row outside the column (or NaN: idamax skips it), else
+// the bits of |a| + 1 (monotone in |a| for non-negative doubles; 1 for an exact zero).  Ties go to
+// the lower row.
+__device__ __forceinline__ unsigned long long piv_key(double a, bool in) {
+  const double f = fabs(a);
+  return (in && f == f) ? (unsigned long long)__double_as_longlong(f) + 1ull : 0ull;
+}
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ unsigned int dpp_max_u32(unsigned int x) {
+  // lanes off the row mask read 0, max's identity: the move folds into v_max_u32_dpp
+  return max(x, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, RM, 0xF, false));
+}
+// the wave's largest u32, uniform: each 16-lane row by quad_perm, half-mirror and mirror, then
+// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the row maxima to lane 63
+__device__ __forceinline__ unsigned int wave_max_u32(unsigned int x) {
+  x = dpp_max_u32<0xB1>(x);
+  x = dpp_max_u32<0x4E>(x);
+  x = dpp_max_u32<0x141>(x);
+  x = dpp_max_u32<0x140>(x);
+  x = dpp_max_u32<0x142, 0xA>(x);
+  x = dpp_max_u32<0x143, 0xC>(x);
+  return (unsigned int)__builtin_amdgcn_readlane((int)x, 63);
+}
+// the wave's largest 64-bit key: the high words, then the low words of the lanes holding that high
+// word (u32 DPP maxima: a 64-bit compare-and-select per step chained VCC through every step)
+__device__ __forceinline__ unsigned long long wave_max_key(unsigned long long k) {
+  const unsigned int h = wave_max_u32((unsigned int)(k >> 32));
+  const unsigned int l = wave_max_u32((unsigned int)(k >> 32) == h ? (unsigned int)k : 0u);
+  return ((unsigned long long)h << 32) | l;
+}
+// the same over each aligned group of NW = 1, 2, 4 or 8 lanes, held by every lane of the group
+template <int NW>
+__device__ __forceinline__ unsigned int group_max_u32(unsigned int x) {
+  if (NW >= 2) x = dpp_max_u32<0xB1>(x);
+  if (NW >= 4) x = dpp_max_u32<0x4E>(x);
+  if (NW >= 8) x = dpp_max_u32<0x141>(x);
+  return x;
+}
+template <int NW>
+__device__ __forceinline__ unsigned long long group_max_key(unsigned long long k) {
+  const unsigned int h = group_max_u32<NW>((unsigned int)(k >> 32));
+  const unsigned int l = group_max_u32<NW>((unsigned int)(k >> 32) == h ? (unsigned int)k : 0u);
+  return ((unsigned long long)h << 32) | l;
+}
+template <int NW>
+__device__ __forceinline__ int group_min_i(int x) {
+  if (NW >= 2) x = min(x, __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));
+  if (NW >= 4) x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x4E, 0xF, 0xF, false));
+  if (NW >= 8) x = min(x, __builtin_amdgcn_update_dpp(x, x, 0x141, 0xF, 0xF, false));
+  return x;
+}
+
+// getf2 on the 16 columns of strip k, rows top .. n_p - 1, held by NW waves in registers: v[r][*]
+// of lane l of wave w is row row0 + rstride r + l (row0 per wave).  The loop is rolled and the rows
+// rotate (an unrolled loop's code is fetched cold on every launch: instruction fetch, not
+// arithmetic, set the time): at column j, v[r][0] is column j, v[r][c] column j + c for c < 16 - j,
+// and v[r][16 - j + i] the finished column i; sixteen rotations restore the natural order.
+// Per column:
+//   * each wave's pivot candidate: the key of |a| (piv_key: 0 for rows above g0 = top + j, past n_p,
+//     or NaN, which idamax skips), the wave maximum by u32 DPP maxima, and the wave's lowest row
+//     holding it by one ballot per register (the rows of a register rise with the lane, registers
+//     with r);
+//   * the wave publishes (key, row, the row's 16 entries, 1 / its entry) into a buffer
+//     alternating by column parity, the owner of row g0 its row; ONE barrier;
+//   * the NW candidates reduced by an NW-lane butterfly (maximum, then the lowest row among the
+//     waves holding it: getrf's first largest |a|), the pivot row read, the swap, the scaling by the
+//     reciprocal and the rank-1 update -- branch-free, the finished columns masked out of the pivot
+//     row (they hold L, not live entries).
+// Pivot choice, reciprocal and FMAs are those of LAPACK's getf2 (and of the round-4 loop: bit-
+// identical factors, up to the sign of an exact zero in a finished column).  Returns true if a
+// column had no nonzero candidate (no swap and no scaling there; the slot reports it singular).
+// ABL (scripts/ubench/lu_panel_ubench.hip only; 0 in the library): parts of the column step left
+// out, to time the rest -- 1 the barrier, 2 the wave reduction, 4 the cross-wave reduction, 8 the
+// update, 16 the swap, 32 the reciprocal, 64 the finished columns' mask; 128: the update without
+// the row branch (the multiplier zeroed on inactive rows).
+template <int NW, int RPL, int ABL = 0>
+__device__ bool panel_columns(StripLds& L, double (&v)[RPL][LB], long long row0, int rstride, int top, int n_p,
+                              int k) {
+  const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) & (NW - 1);
+  long long row[RPL];
 #pragma unroll
-  for (int r = 0; r < LR; ++r) {
-    const long long row = own_row(base, r);
-    if (row >= top && row < g.n_p) {
-#pragma unroll
-      for (int c = 0; c < LB; ++c) P[c * SP_ROWS + (row - top)] = w[r][c];
-    } else if (row < top) {
-#pragma unroll
-      for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + row] = w[r][c];
-    }
-  }
-  __syncthreads();
-  if (wave >= SPW) return;                   // s_barrier then counts the SPW waves left
-  double v[SPR][LB];
-  int off[SPR];
-#pragma unroll
-  for (int r = 0; r < SPR; ++r) {
-    off[r] = wave * 64 * SPR + 64 * r + lane;
-#pragma unroll
-    for (int c = 0; c < LB; ++c) v[r][c] = off[r] < R ? P[c * SP_ROWS + off[r]] : 0.0;
-  }
+  for (int r = 0; r < RPL; ++r) row[r] = row0 + (long long)rstride * r + lane;
   bool singular = false;
-  // rolled, with the rows rotated as in the 8-wave loop (lu_step_kernel)
+  (void)k;
 #pragma unroll 1
   for (int j = 0; j < LB; ++j) {
     const int bf = j & 1;
+    const long long g0 = (long long)top + j;
     LU_CSTAMP(k, j, 0);
-    unsigned long long bk = 0ull;
-    int bo = 0x7fffffff;
+    unsigned long long key[RPL], mk = 0ull;
+    double bv = 1.0;
 #pragma unroll
-    for (int r = 0; r < SPR; ++r) {
-      const unsigned long long kr = piv_key(v[r][0], off[r] >= j && off[r] < R);
-      if (kr > bk) { bk = kr; bo = off[r]; }                   // first max per lane
+    for (int r = 0; r < RPL; ++r) {
+      key[r] = piv_key(v[r][0], row[r] >= g0 && row[r] < n_p);
+      if (key[r] > mk) { mk = key[r]; bv = v[r][0]; }           // the lane's first largest
     }
-    unsigned long long wk;
-    int wo;
-    piv_wave_best(bk, bo, wk, wo);
+    double brp = (ABL & 32) ? bv : 1.0 / bv;                     // in flight under the reduction
+    asm volatile("" : "+v"(brp));                                // (not sunk into the publish)
+    const unsigned long long gk = (ABL & 2) ? bo_readlane_u(mk, 0) : wave_max_key(mk);
+    unsigned long long wm = 0ull;
+    int wr = 0;
+#pragma unroll
+    for (int r = RPL - 1; r >= 0; --r) {
+      const unsigned long long m = __ballot(key[r] == gk);
+      if (m) { wm = m; wr = r; }
+    }
+    const bool has = gk != 0ull;
+    const int wl = (int)__builtin_ctzll(wm | (1ull << 63));
     LU_CSTAMP(k, j, 1);
 #pragma unroll
-    for (int r = 0; r < SPR; ++r)
-      if (wk != 0ull && off[r] == wo) {
+    for (int r = 0; r < RPL; ++r)
+      if (has && r == wr && lane == wl) {
 #pragma unroll
-        for (int c = 0; c < LB; c += 2) *(d2*)&L.cand[bf][wave][c] = (d2){v[r][c], v[r][c + 1]};
+        for (int c = 0; c < LB; c += 2) *(d2*)&L.cand[bf][wv][c] = (d2){v[r][c], v[r][c + 1]};
+        L.crp[bf][wv] = brp;
       }
     if (lane == 0) {
-      L.ck[bf][wave] = wk;
-      L.cr[bf][wave] = wk != 0ull ? wo : 0x7fffffff;
+      L.ck[bf][wv] = gk;
+      L.cr[bf][wv] = has ? (int)(row0 + (long long)rstride * wr + wl) : 0x7fffffff;
     }
-    if (wave == 0 && lane == j) {                              // row 16 k + j: offset j, slot 0
 #pragma unroll
-      for (int c = 0; c < LB; c += 2) *(d2*)&L.grow[bf][c] = (d2){v[0][c], v[0][c + 1]};
-    }
-    __syncthreads();
+    for (int r = 0; r < RPL; ++r)
+      if (row[r] == g0) {
+#pragma unroll
+        for (int c = 0; c < LB; c += 2) *(d2*)&L.grow[bf][c] = (d2){v[r][c], v[r][c + 1]};
+      }
+    if (!(ABL & 1)) __syncthreads();
     LU_CSTAMP(k, j, 2);
-    const unsigned long long k0 = L.ck[bf][0], k1 = L.ck[bf][1];
-    const int r0 = L.cr[bf][0], r1 = L.cr[bf][1];
-    const bool t1 = piv_before(k1, r1, k0, r0);
-    const unsigned long long pk = t1 ? k1 : k0;
-    int po = t1 ? r1 : r0, pw = t1 ? 1 : 0;
-    if (pk <= 1ull) { singular = true; po = j; pw = -1; }       // zero / NaN column: no swap
+    const int u = lane & (NW - 1);
+    const unsigned long long cku = L.ck[bf][u];
+    const int cru = L.cr[bf][u];
+    const unsigned long long G = (ABL & 4) ? cku : group_max_key<NW>(cku);
+    const int pmin = (ABL & 4) ? cru : group_min_i<NW>(cku == G ? cru : 0x7fffffff);
+    const unsigned long long pwm = __ballot(lane < NW && cru == pmin);
+    const unsigned long long Gu = bo_readlane_u(G, 0);
+    const bool zero = Gu <= 1ull;                                // all zero, or no candidate
+    const int p = zero ? (int)g0 : __builtin_amdgcn_readlane(pmin, 0);
+    const int pw = zero ? -1 : (int)__builtin_ctzll(pwm | (1ull << 63));
+    singular = singular || zero;
+    if (threadIdx.x == 0) L.piv[j] = p;
     const double* prow = pw >= 0 ? L.cand[bf][pw] : L.grow[bf];
-    if (tid == 0) L.piv[j] = top + po;
     double pr[LB];
 #pragma unroll
     for (int c = 0; c < LB; c += 2) {
@@ -459,16 +495,14 @@ __device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, dou
       pr[c] = x.x;
       pr[c + 1] = x.y;
     }
-    const double rp = 1.0 / pr[0];
-    const int live = LB - j;
-    double l[SPR];
-    bool act[SPR];
+    const double rp = pw >= 0 ? L.crp[bf][pw] : 0.0;
 #pragma unroll
-    for (int r = 0; r < SPR; ++r) {
-      if (off[r] == j) {
+    for (int r = 0; r < RPL; ++r) {
+      if (ABL & 16) {
+      } else if (row[r] == g0) {
 #pragma unroll
         for (int c = 0; c < LB; ++c) v[r][c] = pr[c];
-      } else if (off[r] == po) {
+      } else if (row[r] == p) {
 #pragma unroll
         for (int c = 0; c < LB; c += 2) {
           const d2 x = *(const d2*)&L.grow[bf][c];
@@ -476,26 +510,68 @@ __device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, dou
           v[r][c + 1] = x.y;
         }
       }
-      act[r] = off[r] > j && off[r] < R;
-      l[r] = v[r][0] * rp;
-      if (act[r]) v[r][0] = l[r];
+    }
+    const int live = LB - j;                                     // rotated columns 1 .. live - 1
+#pragma unroll
+    for (int c = 1; c < LB; ++c) {                               // (after the swap: in place)
+      // a bitwise AND with a uniform mask (~0 iff c < live): per-column selects on VCC serialised
+      // their SALU -> VALU hand-offs (~700 clocks per column)
+      const unsigned int m = (ABL & 64) ? ~0u : (unsigned int)((c - live) >> 31);
+      const unsigned long long b = (unsigned long long)__double_as_longlong(pr[c]);
+      pr[c] = __longlong_as_double((long long)(b & (((unsigned long long)m << 32) | m)));
+    }
+    if constexpr ((ABL & 128) != 0) {
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const bool act = row[r] > g0 && row[r] < n_p;
+        const double l = act ? v[r][0] * rp : 0.0;
+        v[r][0] = act ? l : v[r][0];
+#pragma unroll
+        for (int c = 1; c < LB; ++c) v[r][c] = __builtin_fma(-l, pr[c], v[r][c]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RPL; ++r)
+        if (!(ABL & 8) && row[r] > g0 && row[r] < n_p) {
+          const double l = v[r][0] * rp;
+          v[r][0] = l;
+#pragma unroll
+          for (int c = 1; c < LB; ++c) v[r][c] = __builtin_fma(-l, pr[c], v[r][c]);
+        }
     }
 #pragma unroll
-    for (int c = 1; c < LB; ++c)
-      if (c < live) {
-#pragma unroll
-        for (int r = 0; r < SPR; ++r)
-          if (act[r]) v[r][c] = __builtin_fma(-l[r], pr[c], v[r][c]);
-      }
-#pragma unroll
-    for (int r = 0; r < SPR; ++r) {
-      const double t = v[r][0];
+    for (int r = 0; r < RPL; ++r) {
+      const double t = v[r][0];                                  // rotate: column j goes last
 #pragma unroll
       for (int c = 0; c + 1 < LB; ++c) v[r][c] = v[r][c + 1];
       v[r][LB - 1] = t;
     }
     LU_CSTAMP(k, j, 3);
   }
+  return singular;
+}
+
+// The panel of strip k when its rows to factor (16 k .. n_p) number at most 256 RPL: they move
+// through LDS (P, column-major, PR rows) from the workgroup's 8 waves to SPW = 4 waves, one per SIMD,
+// RPL rows per lane in registers (row offset o = 64 RPL wave + 64 r + lane); the other waves end.
+// The column loop is issue-bound (each wave runs the whole pivot selection; measured ~4200 clocks
+// per column with two waves per SIMD), so one wave per SIMD with more rows each is the faster
+// shape.  The rows of step k-1's U block (base .. 16 k) are stored by their threads before the
+// hand-off.
+template <int NW, int RPL, int PR>
+__device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, const double* __restrict__ P,
+                            long long c0, double* __restrict__ A, int* __restrict__ prec, int slot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int top = LB * k, R = g.n_p - top;
+  double v[RPL][LB];
+  int off[RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    off[r] = wave * 64 * RPL + 64 * r + lane;
+#pragma unroll
+    for (int c = 0; c < LB; ++c) v[r][c] = off[r] < R ? P[c * PR + off[r]] : 0.0;
+  }
+  const bool singular = panel_columns<NW, RPL>(L, v, (long long)top + wave * 64 * RPL, 64, top, g.n_p, k);
   if (tid == 0 && singular) bt.status[slot] = 1;
   LU_STAMP(k, 3);
   if (wave == 0) {
@@ -506,7 +582,7 @@ __device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, dou
   }
   LU_STAMP(k, 4);
 #pragma unroll
-  for (int r = 0; r < SPR; ++r)
+  for (int r = 0; r < RPL; ++r)
     if (off[r] < R) {
 #pragma unroll
       for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + top + off[r]] = v[r][c];
@@ -518,7 +594,7 @@ __device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, dou
 template <int LR>
 __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k) {
   __shared__ StripLds L;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, wave = tid >> 6;
   const int slot = blockIdx.y;
   double* __restrict__ A = bt.A[slot];
   int* __restrict__ prec = bt.prec[slot];
@@ -542,135 +618,42 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
   }
   if (k > 0) strip_apply(A, g, prec + (long long)(k - 1) * PREC, k - 1, L, w);
   if (stamp) LU_STAMP(k, 2);
-  // the small panel only where the 8-wave loop holds two rows per thread (N_p in (512, 1024]):
-  // at N = 1024 3.84 -> 3.43 ms per inverse; at N = 512 (one row per thread) it measured 1.40 vs
-  // 1.36 ms (same box) -- the per-column latency (~1.5 us: pivot search, two LDS round trips, the
-  // division, the update) is the same on 2 waves as on 8
-  if constexpr (LR == 2) {
-    __shared__ double P[LB * SP_ROWS];         // the small panel's hand-off (64 KB)
-    if (blockIdx.x == 0 && g.small_panel && g.n_p - LB * k <= SP_ROWS) {   // workgroup-uniform
-      panel_small<LR>(bt, g, k, L, P, w, base, c0, A, prec, slot);
+  // the panel on 4 waves (1 or 2 rows per lane) once its rows fit 512 (LR <= 2) or 256: the
+  // workgroup's rows >= 16 k go through LDS (P, column-major, PR rows), the rows of step k-1's U
+  // block (base .. 16 k) are stored by their threads, waves 4..7 end; the earlier steps of N > 512
+  // run the panel on all 8 waves, LR rows per lane
+  {
+    constexpr int PR = 512;                    // the hand-off's rows (64 KB)
+    __shared__ double P[LB * PR];
+    const int top = LB * k, R = g.n_p - top;
+    // (at N_p <= 512, LR = 1, the hand-off costs more than it saves: 1.18 vs 1.14 ms per inverse,
+    // same box; at N = 1024 / 2048 the small panel wins, 2.75 vs 2.86 / 9.39 vs 9.66 ms)
+    const bool small = LR <= 2 && (g.small_panel == 2 || (g.small_panel == 1 && LR == 2) ||
+                                   (g.small_panel == 3 && R <= 256));
+    if (blockIdx.x == 0 && small && R <= 512) {   // workgroup-uniform
+#pragma unroll
+      for (int r = 0; r < LR; ++r) {
+        const long long row = own_row(base, r);
+        if (row >= top && row < g.n_p) {
+#pragma unroll
+          for (int c = 0; c < LB; ++c) P[c * PR + (row - top)] = w[r][c];
+        } else if (row < top) {
+#pragma unroll
+          for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + row] = w[r][c];
+        }
+      }
+      __syncthreads();
+      if (wave >= SPW) return;                 // s_barrier then counts the SPW waves left
+      // (4 rows per lane, for 1024 rows, would spill: the rows, the pivot row and the swap's
+      // loads need ~100 + 45 RPL VGPRs)
+      if (R <= 256) panel_small<SPW, 1, PR>(bt, g, k, L, P, c0, A, prec, slot);
+      else if constexpr (LR <= 2) panel_small<SPW, 2, PR>(bt, g, k, L, P, c0, A, prec, slot);
       return;
     }
   }
   if (blockIdx.x == 0) {
-    // factor strip k: columns j, pivot rows g0 = 16 k + j.  A ROLLED loop (the unrolled one was
-    // ~60 KB of code run once per launch: instruction fetch, not arithmetic, set its 36 us), so
-    // the rows rotate instead of being indexed by j: at column j, w[r][0] is column j, w[r][c] is
-    // column j + c for c < 16 - j, and w[r][16 - j + i] is the finished column i.  Sixteen
-    // rotations restore the natural order.
-    bool singular = false;
-#pragma unroll 1
-    for (int j = 0; j < LB; ++j) {
-      const int bf = j & 1;
-      const long long g0 = (long long)LB * k + j;
-      LU_CSTAMP(k, j, 0);
-      unsigned long long bk = 0ull;
-      int brow = 0x7fffffff;
-      // every row's reciprocal (getf2 scales by 1 / pivot), issued before the wave reduction so
-      // that the division's latency overlaps it instead of following it
-      double rcp[LR];
-#pragma unroll
-      for (int r = 0; r < LR; ++r) rcp[r] = 1.0 / w[r][0];
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const long long row = own_row(base, r);
-        const unsigned long long kr = piv_key(w[r][0], row >= g0 && row < g.n_p);
-        if (kr > bk) { bk = kr; brow = (int)row; }                   // first max per thread
-      }
-      unsigned long long wk;
-      int wrow;
-      piv_wave_best(bk, brow, wk, wrow);
-      LU_CSTAMP(k, j, 1);
-      // the wave's pivot candidate row and its reciprocal
-#pragma unroll
-      for (int r = 0; r < LR; ++r)
-        if (wk != 0ull && own_row(base, r) == wrow) {
-#pragma unroll
-          for (int c = 0; c < LB; c += 2) *(d2*)&L.cand[bf][wave][c] = (d2){w[r][c], w[r][c + 1]};
-          L.crp[bf][wave] = rcp[r];
-        }
-      if (lane == 0) {
-        L.ck[bf][wave] = wk;
-        L.cr[bf][wave] = wk != 0ull ? wrow : 0x7fffffff;
-      }
-#pragma unroll
-      for (int r = 0; r < LR; ++r)
-        if (own_row(base, r) == g0) {
-#pragma unroll
-          for (int c = 0; c < LB; c += 2) *(d2*)&L.grow[bf][c] = (d2){w[r][c], w[r][c + 1]};
-          L.grp[bf] = rcp[r];
-        }
-      __syncthreads();
-      LU_CSTAMP(k, j, 2);
-      unsigned long long kk[LW];
-      int rr[LW], ww[LW];
-#pragma unroll
-      for (int u = 0; u < LW; ++u) { kk[u] = L.ck[bf][u]; rr[u] = L.cr[bf][u]; ww[u] = u; }
-      // the workgroup's pivot: a 3-level tree over the 8 wave candidates (depth 3, not 7)
-#pragma unroll
-      for (int h = LW / 2; h >= 1; h >>= 1)
-#pragma unroll
-        for (int u = 0; u < h; ++u) {
-          const bool t = piv_before(kk[u + h], rr[u + h], kk[u], rr[u]);
-          kk[u] = t ? kk[u + h] : kk[u];
-          rr[u] = t ? rr[u + h] : rr[u];
-          ww[u] = t ? ww[u + h] : ww[u];
-        }
-      const unsigned long long pk = kk[0];
-      int p = rr[0], pw = ww[0];
-      // pk - 1 = bits of |pivot|: a zero (or NaN-only) column is singular
-      const bool zero = pk <= 1ull;
-      if (zero) { singular = true; p = (int)g0; pw = -1; }           // zero / NaN column: no swap
-      const double* prow = pw >= 0 ? L.cand[bf][pw] : L.grow[bf];
-      if (tid == 0) L.piv[j] = p;
-      // the pivot row in registers first: every LDS read in flight at once (a read per updated
-      // column inside the branch chain below serialised 15 LDS round trips per column)
-      double pr[LB];
-#pragma unroll
-      for (int c = 0; c < LB; c += 2) {
-        const d2 v = *(const d2*)(prow + c);
-        pr[c] = v.x;
-        pr[c + 1] = v.y;
-      }
-      const double rp = pw >= 0 ? L.crp[bf][pw] : L.grp[bf];
-      const int live = LB - j;                        // rotated columns 1 .. live - 1 are updated
-      double l[LR];
-      bool act[LR];
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const long long row = own_row(base, r);
-        if (row == g0) {
-#pragma unroll
-          for (int c = 0; c < LB; ++c) w[r][c] = pr[c];
-        } else if (row == p) {
-#pragma unroll
-          for (int c = 0; c < LB; c += 2) {
-            const d2 v = *(const d2*)&L.grow[bf][c];
-            w[r][c] = v.x;
-            w[r][c + 1] = v.y;
-          }
-        }
-        act[r] = row > g0 && row < g.n_p;
-        l[r] = w[r][0] * rp;
-        if (act[r]) w[r][0] = l[r];
-      }
-#pragma unroll
-      for (int c = 1; c < LB; ++c)
-        if (c < live) {
-#pragma unroll
-          for (int r = 0; r < LR; ++r)
-            if (act[r]) w[r][c] = __builtin_fma(-l[r], pr[c], w[r][c]);
-        }
-#pragma unroll
-      for (int r = 0; r < LR; ++r) {
-        const double t = w[r][0];                     // rotate: column j goes last
-#pragma unroll
-        for (int c = 0; c + 1 < LB; ++c) w[r][c] = w[r][c + 1];
-        w[r][LB - 1] = t;
-      }
-      LU_CSTAMP(k, j, 3);
-    }
+    // factor strip k on the workgroup's 8 waves (row own_row(base, r) = base + 64 wave + lane + LT r)
+    const bool singular = panel_columns<LW, LR>(L, w, (long long)base + 64 * wave, LT, LB * k, g.n_p, k);
     if (tid == 0 && singular) bt.status[slot] = 1;
     __syncthreads();                                  // L.piv complete
     LU_STAMP(k, 3);
@@ -1056,10 +1039,12 @@ LuGeo make_lu_geo(int n) {
   g.n_p = (n + LB - 1) / LB * LB;
   g.nbs = g.n_p / LB;
   g.Na = g.n_p;
-  // BO_LU_PANEL=wide: every panel on the 8-wave loop (A/B only)
+  // BO_LU_PANEL=wide: every panel on the 8-wave loop; =small: the 4-wave panel at N <= 512 too
+  // (A/B only)
   static const int small = [] {
     const char* e = getenv("BO_LU_PANEL");
-    return (e && strcmp(e, "wide") == 0) ? 0 : 1;
+    return (e && strcmp(e, "wide") == 0) ? 0 : (e && strcmp(e, "small") == 0) ? 2 :
+           (e && strcmp(e, "small256") == 0) ? 3 : 1;
   }();
   g.small_panel = small;
   return g;
@@ -1112,11 +1097,14 @@ int bo_lu_inverse(double* const* out, const double* const* km, int n_lu, int64_t
   BO_CHECK_HIP(hipMemsetAsync(bt.status, 0, sizeof(int) * BO_MAX_OBJ, s));
   const unsigned tiles = (unsigned)((g.n_p + 31) / 32);
   hipLaunchKernelGGL(lu_init_kernel, dim3(tiles, tiles, n_lu), dim3(256), 0, s, bt, g, (long long)ld, jitter);
-  // rows per thread: the fewest that hold N_p (at N = 512 one row, so no predicated-off rows)
+  // rows per thread: the fewest that hold N_p (at N = 512 one row, so no predicated-off rows);
+  // each step launch holds only the rows from its base (16 (k - 1)) down, so it takes the fewest
+  // that hold those (N = 2048: 4 rows per thread for the first 97 steps, then 2, then 1)
   const int lr = (g.n_p + LT - 1) / LT;
-  auto step = lr == 1 ? lu_step_kernel<1> : lr == 2 ? lu_step_kernel<2> : lu_step_kernel<4>;
   for (int k = 0; k < g.nbs; ++k) {
     const int blocks = k > 0 ? g.nbs - k : 1;      // the panel + the strips right of it
+    const int rows = g.n_p - (k > 0 ? LB * (k - 1) : 0);
+    auto step = rows <= LT ? lu_step_kernel<1> : rows <= 2 * LT ? lu_step_kernel<2> : lu_step_kernel<4>;
     hipLaunchKernelGGL(step, dim3(blocks, n_lu), dim3(LT), 0, s, bt, g, k);
   }
   const int nbw = (g.nbs + 7) / 8;
@@ -1164,6 +1152,14 @@ extern "C" __attribute__((visibility("default"))) int bo_debug_lu_cols(long long
   if (n > 64 * LB_DIAG * 4) n = 64 * LB_DIAG * 4;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_lu_cstamp), sizeof(long long) * n) != hipSuccess) return -1;
+  return n;
+}
+
+// the shader-clock stamps taken with them (same layout)
+extern "C" __attribute__((visibility("default"))) int bo_debug_lu_cclk(long long* out, int n) {
+  if (n > 64 * LB_DIAG * 4) n = 64 * LB_DIAG * 4;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_lu_cclk), sizeof(long long) * n) != hipSuccess) return -1;
   return n;
 }
 #endif

@@ -61,3 +61,16 @@ if hasattr(lib, "bo_debug_lu_cols"):
             b0 = (k * 16 + j) * 4
             nxt = cb[b0 + 4] if j < 15 else cb[b0 + 3]
             print("  col", j, " ".join(f"{(cb[b0 + t] - cb[b0]) * 0.01:.2f}" for t in (1, 2, 3)), f"{(nxt - cb[b0]) * 0.01:.2f}")
+if hasattr(lib, "bo_debug_lu_cclk"):
+    import ctypes
+    cw = (ctypes.c_longlong * 4096)()
+    cc = (ctypes.c_longlong * 4096)()
+    lib.bo_debug_lu_cols(cw, 4096)
+    lib.bo_debug_lu_cclk(cc, 4096)
+    for k in (0, 1, 2, 16, 30):
+        b0, b1 = (k * 16) * 4, (k * 16 + 15) * 4 + 3
+        dw, dc = (cw[b1] - cw[b0]) * 10e-9, cc[b1] - cc[b0]
+        if dw > 0:
+            print(f"panel step {k}: {dw*1e6:.2f} us wall, {dc} shader clocks -> {dc/dw/1e9:.3f} GHz; "
+                  f"per column {dc/16:.0f} clocks [" + " ".join(
+                      f"{cc[(k*16+j)*4+t]-cc[(k*16+j)*4+t-1]}" for j in (0, 8) for t in (1, 2, 3)) + "]")
