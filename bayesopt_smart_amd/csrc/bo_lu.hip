@@ -574,6 +574,13 @@ __device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, con
   const bool singular = panel_columns<NW, RPL>(L, v, (long long)top + wave * 64 * RPL, 64, top, g.n_p, k);
   if (tid == 0 && singular) bt.status[slot] = 1;
   LU_STAMP(k, 3);
+  // the factored rows first (the stores drain while wave 0 builds the permutation record)
+#pragma unroll
+  for (int r = 0; r < RPL; ++r)
+    if (off[r] < R) {
+#pragma unroll
+      for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + top + off[r]] = v[r][c];
+    }
   if (wave == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       // L.piv (lane 0) to the wave
     __builtin_amdgcn_wave_barrier();
@@ -581,12 +588,6 @@ __device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, con
     build_perm(L, k, prec + (long long)k * PREC);
   }
   LU_STAMP(k, 4);
-#pragma unroll
-  for (int r = 0; r < RPL; ++r)
-    if (off[r] < R) {
-#pragma unroll
-      for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + top + off[r]] = v[r][c];
-    }
 }
 
 // Launch k: block 0 = panel (strip k), blocks 1.. = strips k + 1 .. (update of step k-1);
@@ -655,10 +656,22 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
     // factor strip k on the workgroup's 8 waves (row own_row(base, r) = base + 64 wave + lane + LT r)
     const bool singular = panel_columns<LW, LR>(L, w, (long long)base + 64 * wave, LT, LB * k, g.n_p, k);
     if (tid == 0 && singular) bt.status[slot] = 1;
-    __syncthreads();                                  // L.piv complete
     LU_STAMP(k, 3);
-    if (wave == 0) build_perm(L, k, prec + (long long)k * PREC);
+#pragma unroll
+    for (int r = 0; r < LR; ++r) {                    // the factored rows first (they drain while
+      const long long row = own_row(base, r);         // wave 0 builds the permutation record)
+      if (row >= g.n_p) continue;
+#pragma unroll
+      for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + row] = w[r][c];
+    }
+    if (wave == 0) {                                  // L.piv: written by lane 0 of this wave
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      build_perm(L, k, prec + (long long)k * PREC);
+    }
     LU_STAMP(k, 4);
+    return;
   }
 #pragma unroll
   for (int r = 0; r < LR; ++r) {
