@@ -38,7 +38,25 @@ def fit():
     torch.cuda.synchronize()
 
 
-res = {k: [] for k in ("back_to_back", "sleep5ms", "after_fit", "sleep20ms")}
+# the loop's state: fitted-like length scales (680) and K^-1 from the device LU path
+km2 = torch.zeros((2, n, n), dtype=torch.float64, device=dev)
+bo.kernels.update_k(km2, xd, 0, n, pv, np.full(2, 680.0))
+kd680 = bo.kernels.invert_k(n, km2, lu_hint=[True, True]).contiguous()
+call680 = bo.predict_acquire(xd, yd, kd680, cands, pm, pv, np.full(2, 680.0), betas, outputs=("mu", "var", "acq"),
+                             topq=3, prepare=True)
+
+
+def timed680():
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    call680()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b)
+
+
+res = {k: [] for k in ("back_to_back", "sleep5ms", "after_fit", "sleep20ms", "ls680_back_to_back",
+                       "ls680_after_fit")}
 call()
 torch.cuda.synchronize()
 for rnd in range(6):
@@ -50,5 +68,9 @@ for rnd in range(6):
     res["after_fit"].append(timed())
     time.sleep(0.02)
     res["sleep20ms"].append(timed())
+    call680()
+    res["ls680_back_to_back"].append(timed680())
+    fit()
+    res["ls680_after_fit"].append(timed680())
 for k, v in res.items():
     print(f"{k:14s} median {np.median(v):.3f} ms  all {' '.join(f'{t:.2f}' for t in v)}", flush=True)
