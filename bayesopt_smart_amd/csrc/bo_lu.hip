@@ -422,39 +422,66 @@ __device__ __forceinline__ int group_min_i(int x) {
 // out, to time the rest -- 1 the barrier, 2 the wave reduction, 4 the cross-wave reduction, 8 the
 // update, 16 the swap, 32 the reciprocal, 64 the finished columns' mask; 128: the update without
 // the row branch (the multiplier zeroed on inactive rows).
+// A wave's pivot candidate for the column held in v[r][CI] (rows >= gmin and < n_p): the maximum
+// key, the first register and lane holding it, and the reciprocal of the lane's first largest
+// entry (computed before the reduction so that its latency overlaps it).
+struct ColSearch {
+  unsigned long long gk;
+  int wr, wl;
+  double brp;
+};
+template <int RPL, int CI, int ABL>
+__device__ __forceinline__ void col_search(const double (&v)[RPL][LB], const long long (&row)[RPL], long long gmin,
+                                           int n_p, ColSearch& s) {
+  unsigned long long key[RPL], mk = 0ull;
+  double bv = 1.0;
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    key[r] = piv_key(v[r][CI], row[r] >= gmin && row[r] < n_p);
+    if (key[r] > mk) { mk = key[r]; bv = v[r][CI]; }              // the lane's first largest
+  }
+  double brp = (ABL & 32) ? bv : 1.0 / bv;                        // in flight under the reduction
+  asm volatile("" : "+v"(brp));                                   // (not sunk into the publish)
+  s.brp = brp;
+  s.gk = (ABL & 2) ? bo_readlane_u(mk, 0) : wave_max_key(mk);
+  unsigned long long wm = 0ull;
+  int wr = 0;
+#pragma unroll
+  for (int r = RPL - 1; r >= 0; --r) {
+    const unsigned long long m = __ballot(key[r] == s.gk);
+    if (m) { wm = m; wr = r; }
+  }
+  s.wr = wr;
+  s.wl = (int)__builtin_ctzll(wm | (1ull << 63));
+}
+
+// PIPE (the default for <= 2 rows per lane; ABL 256 forces it, 512 turns it off): the next
+// column's search issued right after that column's update, ahead of the other columns' FMAs
+// (branch-free update: the multiplier is 0 on inactive rows), so that its DPP chain overlaps them
+// -- per column 3,207 -> 2,912 clocks at 4 waves x 2 rows, 3,073 -> 2,964 at 8 x 1; at 4 rows per
+// lane the branch-free form spills (18,208 clocks) and the row branch stays.
 template <int NW, int RPL, int ABL = 0>
 __device__ bool panel_columns(StripLds& L, double (&v)[RPL][LB], long long row0, int rstride, int top, int n_p,
                               int k) {
+  constexpr bool PIPE = (ABL & 256) != 0 || (RPL <= 2 && (ABL & 512) == 0);
   const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) & (NW - 1);
   long long row[RPL];
 #pragma unroll
   for (int r = 0; r < RPL; ++r) row[r] = row0 + (long long)rstride * r + lane;
   bool singular = false;
   (void)k;
+  ColSearch cs;
+  if constexpr (PIPE) col_search<RPL, 0, ABL>(v, row, top, n_p, cs);
 #pragma unroll 1
   for (int j = 0; j < LB; ++j) {
     const int bf = j & 1;
     const long long g0 = (long long)top + j;
     LU_CSTAMP(k, j, 0);
-    unsigned long long key[RPL], mk = 0ull;
-    double bv = 1.0;
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      key[r] = piv_key(v[r][0], row[r] >= g0 && row[r] < n_p);
-      if (key[r] > mk) { mk = key[r]; bv = v[r][0]; }           // the lane's first largest
-    }
-    double brp = (ABL & 32) ? bv : 1.0 / bv;                     // in flight under the reduction
-    asm volatile("" : "+v"(brp));                                // (not sunk into the publish)
-    const unsigned long long gk = (ABL & 2) ? bo_readlane_u(mk, 0) : wave_max_key(mk);
-    unsigned long long wm = 0ull;
-    int wr = 0;
-#pragma unroll
-    for (int r = RPL - 1; r >= 0; --r) {
-      const unsigned long long m = __ballot(key[r] == gk);
-      if (m) { wm = m; wr = r; }
-    }
+    if constexpr (!PIPE) col_search<RPL, 0, ABL>(v, row, g0, n_p, cs);
+    const unsigned long long gk = cs.gk;
+    const int wr = cs.wr, wl = cs.wl;
+    const double brp = cs.brp;
     const bool has = gk != 0ull;
-    const int wl = (int)__builtin_ctzll(wm | (1ull << 63));
     LU_CSTAMP(k, j, 1);
 #pragma unroll
     for (int r = 0; r < RPL; ++r)
@@ -520,7 +547,21 @@ __device__ bool panel_columns(StripLds& L, double (&v)[RPL][LB], long long row0,
       const unsigned long long b = (unsigned long long)__double_as_longlong(pr[c]);
       pr[c] = __longlong_as_double((long long)(b & (((unsigned long long)m << 32) | m)));
     }
-    if constexpr ((ABL & 128) != 0) {
+    if constexpr (PIPE) {
+      double l[RPL];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const bool act = row[r] > g0 && row[r] < n_p;
+        l[r] = act ? v[r][0] * rp : 0.0;
+        v[r][0] = act ? l[r] : v[r][0];
+        v[r][1] = __builtin_fma(-l[r], pr[1], v[r][1]);
+      }
+      col_search<RPL, 1, ABL>(v, row, g0 + 1, n_p, cs);           // (at j = 15: unused)
+#pragma unroll
+      for (int r = 0; r < RPL; ++r)
+#pragma unroll
+        for (int c = 2; c < LB; ++c) v[r][c] = __builtin_fma(-l[r], pr[c], v[r][c]);
+    } else if constexpr ((ABL & 128) != 0) {
 #pragma unroll
       for (int r = 0; r < RPL; ++r) {
         const bool act = row[r] > g0 && row[r] < n_p;

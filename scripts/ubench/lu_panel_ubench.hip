@@ -55,16 +55,16 @@ int main() {
   (void)hipMalloc(&clk, 64);
   (void)hipMemcpy(A, h, sizeof(double) * R * LB, hipMemcpyHostToDevice);
 #define ALL(NW, RPL, RR)                                              \
-  run<NW, RPL, 0>(A, RR, clk, "full");                                \
-  run<NW, RPL, 8>(A, RR, clk, "no update");                           \
-  run<NW, RPL, 64>(A, RR, clk, "no finished-column mask");            \
-  run<NW, RPL, 128>(A, RR, clk, "update without row branch");         \
-  run<NW, RPL, 192>(A, RR, clk, "no mask, no row branch");            \
-  run<NW, RPL, 1>(A, RR, clk, "no barrier");                          \
-  run<NW, RPL, 16>(A, RR, clk, "no swap");                            \
-  run<NW, RPL, 63>(A, RR, clk, "all of them out");
+  run<NW, RPL, 0>(A, RR, clk, "library default");                     \
+  run<NW, RPL, 512>(A, RR, clk, "row-branch update");                 \
+  run<NW, RPL, 768>(A, RR, clk, "next search ahead of the update");   \
+  run<NW, RPL, 520>(A, RR, clk, "no update");                         \
+  run<NW, RPL, 513>(A, RR, clk, "no barrier");                        \
+  run<NW, RPL, 575>(A, RR, clk, "all of them out");
   ALL(8, 1, 512)
   ALL(4, 2, 512)
   ALL(4, 1, 256)
+  ALL(8, 2, 512)
+  ALL(8, 4, 512)
   return 0;
 }
