@@ -328,8 +328,31 @@ __device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const 
   r16_start(A, g.Na, base, base, act, st);
   put_perm(L, pm, pp, ps);
   __syncthreads();
-  apply_perm(L, w, base, g.n_p);
-  // L11 (unit lower) and the 16 top rows into LDS
+  // the permutation (apply_perm without its map reset: every launch starts from init_maps), with
+  // L11 (unit lower) and the 16 permuted top rows into LDS in the same phase: four barriers per
+  // strip instead of six
+  const int m = L.m;
+  if (m != 0) {                                      // uniform
+#pragma unroll
+    for (int r = 0; r < LR; ++r) {
+      const long long row = own_row(base, r);
+      const int u = row < g.n_p ? L.smap[row] : -1;
+      if (u >= 0) {
+#pragma unroll
+        for (int c = 0; c < LB; ++c) L.buf[u][c] = w[r][c];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < LR; ++r) {
+      const long long row = own_row(base, r);
+      const int u = row < g.n_p ? L.pmap[row] : -1;
+      if (u >= 0) {
+#pragma unroll
+        for (int c = 0; c < LB; ++c) w[r][c] = L.buf[u][c];
+      }
+    }
+  }
   if (tid < LB * LB) L.L11[tid & 15][tid >> 4] = l11;
   if (tid < LB) {
 #pragma unroll
@@ -343,7 +366,8 @@ __device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const 
     for (int c = 0; c < LB; ++c) w[0][c] = L.T[tid][c];
   }
   r16_finish(A, g.Na, base, L, w, act, st);
-  __syncthreads();                                   // L.T is rewritten by the next phase
+  // (no barrier: nothing later in the launch writes L.T, L.L11 or L.buf -- the panel uses its own
+  // fields, the small panel's hand-off its own array)
 }
 
 // ------------------------------------------------------------- the pivot columns of a panel
