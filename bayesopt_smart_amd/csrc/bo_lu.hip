@@ -310,24 +310,60 @@ __device__ __forceinline__ void r16_finish(const double* __restrict__ A, long lo
   }
 }
 
+// an f64 MFMA's result is read by plain VALU / LDS instructions only after its latency: wait states
+__device__ __forceinline__ void acc_fence(d4& x) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(x));
+}
+
 // Step s applied to a strip whose rows [16 s, n_p) are in registers (base = 16 s): the
 // permutation, U12 = L11^-1 A12 (rows 16 s .. 16 s + 15), A22 -= L21 U12.
+// The rank-16 update's transpose: per wave 64 rows of 16 columns, rows padded to 17 doubles
+constexpr int TPS = LB + 1;
 template <int LR>
 __device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const int* __restrict__ rec, int s,
-                            StripLds& L, double (&w)[LR][LB]) {
-  const int base = LB * s, tid = threadIdx.x;
-  // every global load of the step issued first: the permutation record, L11, the first columns
-  // of L21
+                            const double* __restrict__ tinv_s, StripLds& L, double* __restrict__ tp,
+                            double (&w)[LR][LB]) {
+  const int base = LB * s, tid = threadIdx.x, lane = tid & 63, li = lane & 15, lg = lane >> 4;
+  // every global load of the step issued first: the permutation record, inv(L11) (wave 0: the
+  // MFMA A operand, row li and columns 4 ks + lg; written by the panel of step s), the first
+  // columns of L21
   int pm = 0, pp = 0, ps = 0;
   if (tid < 32) get_perm(rec, pm, pp, ps);
-  const double l11 = tid < LB * LB ? A[(long long)(base + (tid >> 4)) * g.Na + base + (tid & 15)] : 0.0;
+  double tl[4] = {0.0, 0.0, 0.0, 0.0};
+  if (tid < 64) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) tl[ks] = tinv_s[li * LB + 4 * ks + lg];
+  }
   bool act[LR];
 #pragma unroll
   for (int r = 0; r < LR; ++r) act[r] = own_row(base, r) >= base + LB && own_row(base, r) < g.n_p;
+  // the rank-16 update's A operand (L21: rows of this wave's 16-row tiles, columns 4 ks + lg of the
+  // step), row block r = 0 issued now; rows past n_p read row `base` (their result is dropped)
+  const int wave = tid >> 6;
+  auto l21_load = [&](int r, double (&am)[4][4]) {
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      const long long row = (long long)base + LT * r + 64 * wave + 16 * rt + li;
+      const long long rr = row < g.n_p ? row : base;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) am[rt][ks] = A[(long long)(base + 4 * ks + lg) * g.Na + rr];
+    }
+  };
+  // the matrix-core form at 1 and 2 rows per thread; 4 keep the 256-FMA form (two waves per SIMD
+  // share the matrix pipe there: N = 2048 8.47 vs 8.60 ms, same box).  BO_BUILD_VARIANT=
+  // DEF_LU_R16_MFMA4 builds the matrix-core form at 4 too (A/B only).
+#ifdef BO_LU_R16_MFMA4
+  constexpr bool mf = true;
+#else
+  constexpr bool mf = LR < 4;
+#endif
+  double am[4][4];
   R16<LR> st;
-  r16_start(A, g.Na, base, base, act, st);
+  if constexpr (mf) l21_load(0, am);
+  else r16_start(A, g.Na, base, base, act, st);
   put_perm(L, pm, pp, ps);
   __syncthreads();
+  if (blockIdx.x == 0) LU_STAMP(s + 1, 5);          // (diagnostic builds: the panel workgroup's phases)
   // the permutation (apply_perm without its map reset: every launch starts from init_maps), with
   // L11 (unit lower) and the 16 permuted top rows into LDS in the same phase: four barriers per
   // strip instead of six
@@ -353,19 +389,69 @@ __device__ void strip_apply(const double* __restrict__ A, const LuGeo& g, const 
       }
     }
   }
-  if (tid < LB * LB) L.L11[tid & 15][tid >> 4] = l11;
   if (tid < LB) {
 #pragma unroll
     for (int c = 0; c < LB; ++c) L.T[tid][c] = w[0][c];
   }
   __syncthreads();
-  trsm_lower(L);
+  if (blockIdx.x == 0) LU_STAMP(s + 1, 6);
+  // U12 = inv(L11) A12: four MFMAs on wave 0 (B operand T[4 ks + lg][li]; the accumulator holds
+  // U12[lg + 4 i][li]), in place of the 16-lane substitution chain (~1.7 us per step)
+  if (tid < 64) {
+    double tb[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) tb[ks] = L.T[4 * ks + lg][li];
+    d4 u = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) u = __builtin_amdgcn_mfma_f64_16x16x4f64(tl[ks], tb[ks], u, 0, 0, 0);
+    acc_fence(u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) L.T[lg + 4 * i][li] = u[i];
+  }
   __syncthreads();
+  if (blockIdx.x == 0) LU_STAMP(s + 1, 7);
   if (tid < LB) {
 #pragma unroll
     for (int c = 0; c < LB; ++c) w[0][c] = L.T[tid][c];
   }
-  r16_finish(A, g.Na, base, L, w, act, st);
+  // A22 -= L21 U12 on the matrix cores: per wave and row block, four 16-row tiles x four k-steps
+  // (B operand U12[4 ks + lg][li], shared by the tiles), the product transposed to rows through
+  // the wave's LDS block; the round-4 form was 256 FMAs per row against 256 LDS broadcasts
+  if constexpr (!mf) {
+    r16_finish(A, g.Na, base, L, w, act, st);
+    return;
+  }
+  double tb[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) tb[ks] = L.T[4 * ks + lg][li];
+  double* __restrict__ pw = tp + (size_t)wave * 64 * TPS;
+#pragma unroll
+  for (int r = 0; r < LR; ++r) {
+    d4 acc[4];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      acc[rt] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc[rt] = __builtin_amdgcn_mfma_f64_16x16x4f64(am[rt][ks], tb[ks], acc[rt], 0, 0, 0);
+    }
+    if (r + 1 < LR) l21_load(r + 1, am);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) acc_fence(acc[rt]);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pw[(16 * rt + lg + 4 * i) * TPS + li] = acc[rt][i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (act[r]) {
+#pragma unroll
+      for (int c = 0; c < LB; ++c) w[r][c] -= pw[lane * TPS + c];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       // the block is rewritten next
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   // (no barrier: nothing later in the launch writes L.T, L.L11 or L.buf -- the panel uses its own
   // fields, the small panel's hand-off its own array)
 }
@@ -616,6 +702,26 @@ __device__ bool panel_columns(StripLds& L, double (&v)[RPL][LB], long long row0,
   return singular;
 }
 
+// inv(L11) of the step just factored, for the next launch's strip apply (U12 = inv(L11) A12 on the
+// matrix cores instead of a 16-lane substitution): the panel's diagonal rows were staged in L.L11;
+// wave 1 (lanes 0..15, one column each) substitutes on the identity -- the operations of
+// diag_block_inverses, so the finalize kernel later writes the same values -- while wave 0 builds
+// the permutation record.
+__device__ __forceinline__ void l11_inverse_to(const StripLds& L, double* __restrict__ tinv_k) {
+  const int lane = threadIdx.x & 63;
+  if ((threadIdx.x >> 6) != 1 || lane >= LB) return;
+  const int t = lane;
+  double x[LB];
+#pragma unroll
+  for (int i = 0; i < LB; ++i) x[i] = i == t ? 1.0 : 0.0;
+#pragma unroll
+  for (int i = 1; i < LB; ++i)
+#pragma unroll
+    for (int m = 0; m < i; ++m) x[i] = __builtin_fma(-L.L11[i][m], x[m], x[i]);
+#pragma unroll
+  for (int i = 0; i < LB; ++i) tinv_k[i * LB + t] = x[i];
+}
+
 // The panel of strip k when its rows to factor (16 k .. n_p) number at most 256 RPL: they move
 // through LDS (P, column-major, PR rows) from the workgroup's 8 waves to SPW = 4 waves, one per SIMD,
 // RPL rows per lane in registers (row offset o = 64 RPL wave + 64 r + lane); the other waves end.
@@ -639,19 +745,21 @@ __device__ void panel_small(LuBatch& bt, const LuGeo& g, int k, StripLds& L, con
   const bool singular = panel_columns<NW, RPL>(L, v, (long long)top + wave * 64 * RPL, 64, top, g.n_p, k);
   if (tid == 0 && singular) bt.status[slot] = 1;
   LU_STAMP(k, 3);
-  // the factored rows first (the stores drain while wave 0 builds the permutation record)
+  // the factored rows first (the stores drain while wave 0 builds the permutation record and wave
+  // 1 inverts L11); the diagonal rows (offsets 0..15: wave 0, r = 0) staged for wave 1
 #pragma unroll
   for (int r = 0; r < RPL; ++r)
     if (off[r] < R) {
 #pragma unroll
       for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + top + off[r]] = v[r][c];
     }
-  if (wave == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       // L.piv (lane 0) to the wave
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    build_perm(L, k, prec + (long long)k * PREC);
+  if (wave == 0 && lane < LB) {
+#pragma unroll
+    for (int c = 0; c < LB; ++c) L.L11[lane][c] = v[0][c];
   }
+  __syncthreads();                                   // L.piv and the staged rows
+  if (wave == 0) build_perm(L, k, prec + (long long)k * PREC);
+  l11_inverse_to(L, bt.tinv[slot] + (long long)k * 512);
   LU_STAMP(k, 4);
 }
 
@@ -682,7 +790,9 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
 #pragma unroll
     for (int c = 0; c < LB; ++c) w[r][c] = row < g.n_p ? w[r][c] : 0.0;
   }
-  if (k > 0) strip_apply(A, g, prec + (long long)(k - 1) * PREC, k - 1, L, w);
+  __shared__ double TP[LW * 64 * TPS];          // the strip apply's transpose (68 KB)
+  if (k > 0)
+    strip_apply(A, g, prec + (long long)(k - 1) * PREC, k - 1, bt.tinv[slot] + (long long)(k - 1) * 512, L, TP, w);
   if (stamp) LU_STAMP(k, 2);
   // the panel on 4 waves (1 or 2 rows per lane) once its rows fit 512 (LR <= 2) or 256: the
   // workgroup's rows >= 16 k go through LDS (P, column-major, PR rows), the rows of step k-1's U
@@ -729,12 +839,16 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
 #pragma unroll
       for (int c = 0; c < LB; ++c) A[(c0 + c) * g.Na + row] = w[r][c];
     }
-    if (wave == 0) {                                  // L.piv: written by lane 0 of this wave
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      build_perm(L, k, prec + (long long)k * PREC);
+    {                                                 // the diagonal rows (row 16 k + i: thread
+      const int t0 = LB * k - base;                   // t0 + i, r = 0) staged for wave 1
+      if (tid >= t0 && tid < t0 + LB) {
+#pragma unroll
+        for (int c = 0; c < LB; ++c) L.L11[tid - t0][c] = w[0][c];
+      }
     }
+    __syncthreads();                                  // L.piv and the staged rows
+    if (wave == 0) build_perm(L, k, prec + (long long)k * PREC);
+    l11_inverse_to(L, bt.tinv[slot] + (long long)k * 512);
     LU_STAMP(k, 4);
     return;
   }
@@ -859,9 +973,6 @@ __global__ __launch_bounds__(LT) void lu_finalize_kernel(LuBatch bt, LuGeo g) {
 // P e (the blocks above it stay zero), backward over every block.  The previous version held one
 // row per thread and read T as LDS broadcasts (256 per row per step: ~1.7 us of LDS per step at
 // N = 512) with the step's permutation applied through LDS (three barriers per step).
-__device__ __forceinline__ void acc_fence(d4& x) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(x));
-}
 
 // One direction of the solve.  Step s: its owner wave (s & 7) applies the step's triangle to its
 // block, T = tinv_s W_s (four MFMAs: the f64 accumulator layout -- lane (li, lg) holds rows
