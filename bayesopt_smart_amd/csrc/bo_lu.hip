@@ -6,17 +6,18 @@
 // every such objective of one call is factored in the same launches (grid y = the objective).
 //
 // A (N padded to 16 with identity) is column-major in the workspace.  A 16-column STRIP's rows
-// are held up to four per thread of a 512-thread workgroup (16 doubles per row in registers).
-// Launch k (one per 16-column step):
+// are held 1, 2 or 4 per thread of a 512-thread workgroup (16 doubles per row in registers; each
+// step launch takes the fewest that hold its rows).  Launch k (one per 16-column step):
 //   * panel (strip k): applies the pending step k-1 to its strip -- the step's row permutation
-//     (<= 32 rows through LDS), U12 = L11^-1 A12 (16 lanes, each column's substitution chain in
-//     registers) and the rank-16 update of the rows below -- then factors the strip.  Per column
-//     ONE barrier: every wave publishes its best row (value, index and the row's 16 entries: wave
-//     max by shuffles, the lowest row among the lanes holding it by ballots) and the thread holding
-//     row j publishes that row, into a buffer alternating by column parity; after the barrier every
-//     thread picks the pivot among the 8 wave results, swaps and applies the rank-1 update to its
-//     own rows.  Wave 0 then composes the step's 16 swaps into one permutation record (pos <- src
-//     pairs, by ballots over 32 lanes) that every later consumer reads;
+//     (<= 32 rows through LDS), U12 = inv(L11) A12 (four MFMAs; inv(L11) left by step k-1's panel)
+//     and the rank-16 update of the rows below (MFMAs through an LDS transpose at 1-2 rows per
+//     thread) -- then factors the strip (panel_columns, on 8 waves or on 4 after an LDS hand-off).
+//     Per column ONE barrier: every wave publishes its pivot candidate (the u32 DPP maximum of
+//     the |a| keys, the lowest row holding it by ballots, the row's 16 entries), the owner of row
+//     j that row; after the barrier every wave picks the pivot among the wave candidates, swaps and
+//     applies the rank-1 update to its rows, the next column's search issued ahead of the other
+//     columns' FMAs.  Wave 0 then composes the step's 16 swaps into one permutation record (pos <-
+//     src pairs) that every later consumer reads, while wave 1 inverts the new L11;
 //   * update (strips > k): step k-1 applied to each strip by its own workgroup (lookahead: the
 //     panel of step k needs only its own strip).
 // The L columns keep the row order of their own step during the factorisation.  After the last
