@@ -95,7 +95,6 @@ struct LuGeo {
   int n, n_p, nbs;              // N, N padded to 16, strips
   long long Na;                 // leading dimension (= n_p)
   int small_panel;              // 0 never, 1 above N_p = 512, 2 always: the 4-wave panel (panel_small)
-  int xcd_map;                  // 1: the block -> strip map keeps each slot's panel on one XCD
 };
 
 constexpr int SPW = 4;                  // waves of the small panel (one per SIMD)
@@ -774,21 +773,10 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
   const int slot = blockIdx.y;
   double* __restrict__ A = bt.A[slot];
   int* __restrict__ prec = bt.prec[slot];
-  // which strip this block takes (rel 0 = the panel).  Blocks reach the XCDs by linear id mod 8:
-  // with xcd_map the panel of slot y sits at the x whose id is = y (mod 8) every launch, and the
-  // update of strip k + 1 -- the next launch's panel strip -- runs 8 blocks later, on that XCD, so
-  // the next panel's strip, L21, inv(L11) and record are in its L2
-  int rel = (int)blockIdx.x;
-  if (g.xcd_map && gridDim.x > 8) {
-    const int X = (int)gridDim.x, y = (int)blockIdx.y;
-    const int xp = (((y - y * X) % 8) + 8) % 8;
-    rel = ((int)blockIdx.x - xp + X) % X;
-    rel = rel == 8 ? 1 : (rel >= 1 && rel <= 7 ? rel + 1 : rel);
-  }
-  const int strip = k + rel;
+  const int strip = k + (int)blockIdx.x;
   const int base = k > 0 ? LB * (k - 1) : 0;
   const long long c0 = (long long)LB * strip;
-  const bool stamp = rel == 0;
+  const bool stamp = blockIdx.x == 0;
   (void)stamp;
   if (stamp) LU_STAMP(k, 1);
   init_maps(L);
@@ -819,7 +807,7 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
     // same box; at N = 1024 / 2048 the small panel wins, 2.75 vs 2.86 / 9.39 vs 9.66 ms)
     const bool small = LR <= 2 && (g.small_panel == 2 || (g.small_panel == 1 && LR == 2) ||
                                    (g.small_panel == 3 && R <= 256));
-    if (rel == 0 && small && R <= 512) {   // workgroup-uniform
+    if (blockIdx.x == 0 && small && R <= 512) {   // workgroup-uniform
 #pragma unroll
       for (int r = 0; r < LR; ++r) {
         const long long row = own_row(base, r);
@@ -840,7 +828,7 @@ __global__ __launch_bounds__(LT) void lu_step_kernel(LuBatch bt, LuGeo g, int k)
       return;
     }
   }
-  if (rel == 0) {
+  if (blockIdx.x == 0) {
     // factor strip k on the workgroup's 8 waves (row own_row(base, r) = base + 64 wave + lane + LT r)
     const bool singular = panel_columns<LW, LR>(L, w, (long long)base + 64 * wave, LT, LB * k, g.n_p, k);
     if (tid == 0 && singular) bt.status[slot] = 1;
@@ -1249,12 +1237,6 @@ LuGeo make_lu_geo(int n) {
            (e && strcmp(e, "small256") == 0) ? 3 : 1;
   }();
   g.small_panel = small;
-  // BO_LU_XCD=0: the plain block -> strip map (A/B only)
-  static const int xcd = [] {
-    const char* e = getenv("BO_LU_XCD");
-    return (e && strcmp(e, "0") == 0) ? 0 : 1;
-  }();
-  g.xcd_map = xcd;
   return g;
 }
 
