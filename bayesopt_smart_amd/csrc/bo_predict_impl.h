@@ -382,7 +382,8 @@ struct KGen {
 #endif
 // PART (UPPER, N not a multiple of 32): the first chunk each group streams -- the last rows,
 // partly padding -- is peeled and its all-padding k-step pairs skip their MFMAs (their K* rows
-// are exactly 0, so the outputs are bit-identical).  A separate instantiation: the multiples
+// are exactly 0, so the outputs are bit-identical) and, with the 4-deep ring, their W refills
+// (one instantiation per count of live pairs: the refills issued anyway cost N = 518 2 %).  A separate instantiation: the multiples
 // of 32 keep the loop's code layout (peeling it into the one kernel cost C3 1.5 %, C4 3 %).
 template <int DIM, bool SEP, bool UPPER, bool GROWS, int MAXEP, bool PART = false>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
@@ -529,9 +530,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         // regenerates itself (chn clamped) and the groups after the first accumulate a mean
         // that is dropped (msave).
         KGen<DIM, SEP> gen;
+        using K4 = std::integral_constant<int, 4>;
         // kp: the chunk's k-step pairs (8 rows each) that hold a training row (4 unless PART's
         // peeled last chunk)
-        auto chunk_step = [&](int ch, const double (&B)[8], double (&Bn)[8], int kp) {
+        auto chunk_step = [&](auto kp_c, int ch, const double (&B)[8], double (&Bn)[8]) {
+          constexpr int kp = decltype(kp_c)::value;
           double An[8];
           // next chunk: ascending (dense) / descending (upper); the last one regenerates itself
           const int chn = upper ? (ch > e0 ? ch - 1 : ch) : (ch + 1 < nch ? ch + 1 : ch);
@@ -541,6 +544,16 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           // exact; independent guards made every body a join and cost a vmcnt(0) drain of the
           // W ring per E-pair.
           const int n_here = upper ? (ch - e0 + 1 < eN ? ch - e0 + 1 : eN) : eN;
+          // PART's peeled chunk: its bodies neither multiply nor refill the pairs >= kp (all
+          // padding); those ring slots are loaded once, here, with the next chunk's first body
+          // (pairs pos + 4 n_here + s: the chunk's stream keeps 4 pairs per body)
+          if constexpr (PART && PF == 4 && kp < 4) {
+#pragma unroll
+            for (int s = kp; s < 4; ++s) {
+              wa[s] = wload(wr, voff, base + ((pos + 4 * n_here + s) << 11));
+              wb[s] = wload(wr, voff, base + ((pos + 4 * n_here + s) << 11) + 1024);
+            }
+          }
           auto ep_body = [&](auto e_c) {
             constexpr int e = decltype(e_c)::value;
             // explicit / Sobol candidates: keep the workgroup's 4 waves on the same E-pair block
@@ -570,8 +583,10 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               }
               const int so = base + ((pos + PF) << 11);
 #ifndef BO_ABL_NOREFILL
-              wa[sl] = wload(wr, voff, so);
-              wb[sl] = wload(wr, voff, so + 1024);
+              if (!(PART && PF == 4) || pp < kp) {
+                wa[sl] = wload(wr, voff, so);
+                wb[sl] = wload(wr, voff, so + 1024);
+              }
 #else
               (void)so;   // ablation: the primed W values are reused (no W traffic; timing only)
 #endif
@@ -619,25 +634,29 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         int ch = c0;
         if constexpr (PART && UPPER) {
           const int r_last = a.n_train - 32 * (nch - 1);
-          chunk_step(ch, BX, BY, (r_last + 7) >> 3);
+          const int kpv = (r_last + 7) >> 3;
+          if (kpv == 1) chunk_step(std::integral_constant<int, 1>{}, ch, BX, BY);
+          else if (kpv == 2) chunk_step(std::integral_constant<int, 2>{}, ch, BX, BY);
+          else if (kpv == 3) chunk_step(std::integral_constant<int, 3>{}, ch, BX, BY);
+          else chunk_step(K4{}, ch, BX, BY);
           --ch;
           for (; ch - 1 >= e0; ch -= 2) {
-            chunk_step(ch, BY, BX, 4);
-            chunk_step(ch - 1, BX, BY, 4);
+            chunk_step(K4{}, ch, BY, BX);
+            chunk_step(K4{}, ch - 1, BX, BY);
           }
-          if (ch >= e0) chunk_step(ch, BY, BX, 4);
+          if (ch >= e0) chunk_step(K4{}, ch, BY, BX);
         } else if (upper) {
           for (; ch - 1 >= e0; ch -= 2) {
-            chunk_step(ch, BX, BY, 4);
-            chunk_step(ch - 1, BY, BX, 4);
+            chunk_step(K4{}, ch, BX, BY);
+            chunk_step(K4{}, ch - 1, BY, BX);
           }
-          if (ch >= e0) chunk_step(ch, BX, BY, 4);
+          if (ch >= e0) chunk_step(K4{}, ch, BX, BY);
         } else {
           for (; ch + 1 < nch; ch += 2) {
-            chunk_step(ch, BX, BY, 4);
-            chunk_step(ch + 1, BY, BX, 4);
+            chunk_step(K4{}, ch, BX, BY);
+            chunk_step(K4{}, ch + 1, BY, BX);
           }
-          if (ch < nch) chunk_step(ch, BX, BY, 4);
+          if (ch < nch) chunk_step(K4{}, ch, BX, BY);
         }
         // dense: q = k . z after the last chunk, chunk ep's K* regenerated.  Software-pipelined:
         // E-pair e+1's rows are loaded (KGen s0/s1) before E-pair e's fence and multiplied after
