@@ -14,6 +14,7 @@
 #include "bo_common.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -897,7 +898,17 @@ __host__ __device__ inline long long c32_blocks(int nch) {
   return b;
 }
 
-template <int DIM>
+// PART (N not a multiple of 64, at most 48 rows in the last chunk): as in the f64 kernel, the
+// first chunk each group streams -- the last 64 rows, partly padding -- is peeled.  Its k-quads
+// (16 rows each) that hold only padding rows skip their MFMAs, their W refills, the mean's FMAs
+// and the first-chunk generation: those K* rows are exactly 0 (padded rows at inf, exp2f(-inf)),
+// so the outputs are bit-identical.  One KERNEL per count of live k-quads KQV (1..3; 4 = no
+// peel): a runtime switch between the peeled variants inside one kernel spilled 460 B per lane
+// (the joins of 256 accumulators), against 52 B for the unpeeled kernel.  The
+// ring slots the skipped refills would have filled are loaded once, at the chunk's start, with
+// the body after the chunk.  Every loop N of C5 (2064 ... 2240) is such an N: before the peel
+// N = 2049 cost what N = 2112 does (+6.6 % over N = 2048, profiles/r05_c5_fp32_npad_probe.txt).
+template <int DIM, int KQV = 4>
 __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem32[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -937,10 +948,15 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
         for (int k = 0; k < DIM; ++k) { const float d = r[k] - c32[k]; d2 = __builtin_fmaf(d, d, d2); }
         return __builtin_amdgcn_exp2f(__builtin_fmaf(d2, nl2, lpv));
       };
-      auto chunk = [&](int ch, float (&B)[16]) {
+      // the chunk's K* in the permuted k-step order; k-quads >= KQ (all padding) are 0
+      auto chunk_kq = [&](auto kq_c, int ch, float (&B)[16]) {
+        constexpr int KQ = decltype(kq_c)::value;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) B[s] = kval(64 * ch + 16 * (s >> 2) + 4 * g + (s & 3));
+        for (int s = 0; s < 16; ++s)
+          B[s] = (s >> 2) < KQ ? kval(64 * ch + 16 * (s >> 2) + 4 * g + (s & 3)) : 0.0f;
       };
+      using Q4 = std::integral_constant<int, 4>;
+      auto chunk = [&](int ch, float (&B)[16]) { chunk_kq(Q4{}, ch, B); };
       const float* alo = al + (size_t)o * a.n_pad;
       const int base = (int)(o * w_obj);
       f4 w[16];
@@ -955,9 +971,19 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
         for (int e = 0; e < kC32MaxEp; ++e)
 #pragma unroll
           for (int b = 0; b < 4; ++b) acc[e][b] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
-        auto chunk_step = [&](int ch, const float (&B)[16], float (&Bn)[16]) {
+        // kqv: the chunk's k-quads that hold a training row (4 unless PART's peeled last chunk)
+        auto chunk_step = [&](auto kq_c, int ch, const float (&B)[16], float (&Bn)[16]) {
+          constexpr int kqv = decltype(kq_c)::value;
           const int chn = ch > e0 ? ch - 1 : ch;
           const int n_here = ch - e0 + 1 < eN ? ch - e0 + 1 : eN;
+          if constexpr (kqv < 4) {
+            // the ring slots of the skipped k-quads: the body after this chunk's n_here bodies
+#pragma unroll
+            for (int kq = kqv; kq < 4; ++kq)
+#pragma unroll
+              for (int b = 0; b < 4; ++b)
+                w[4 * kq + b] = wload32(wr, voff, base + (pos + n_here) * 16384 + kq * 4096 + b * 1024);
+          }
           auto ep_body = [&](auto e_c) {
             constexpr int e = decltype(e_c)::value;
             // keep the workgroup's 4 waves on the same E-quad block: they stream identical W
@@ -967,14 +993,14 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
             if constexpr (e == 0) {
               // branch-free (a join here would drain the W ring with vmcnt(0))
 #pragma unroll
-              for (int s = 0; s < 16; ++s) {
+              for (int s = 0; s < 4 * kqv; ++s) {
                 const float av = alo[64 * ch + 16 * (s >> 2) + 4 * g + (s & 3)];
                 mpart = __builtin_fmaf(av, B[s], mpart);   // group 0's is kept (msave)
               }
               chunk(chn, Bn);
             }
 #pragma unroll
-            for (int kq = 0; kq < 4; ++kq) {
+            for (int kq = 0; kq < kqv; ++kq) {
 #pragma unroll
               for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -987,7 +1013,7 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
             if (ch - e0 == e) {
               mfma_fence32(acc[e][0], acc[e][1], acc[e][2], acc[e][3]);
 #pragma unroll
-              for (int b = 0; b < 4; ++b)
+              for (int b = 0; b < kqv; ++b)       // blocks b >= kqv: B rows of padding (0)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) qpart = __builtin_fmaf(B[4 * b + r], acc[e][b][r], qpart);
             }
@@ -995,13 +1021,25 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
           EpChain<0, kC32MaxEp>::run(ep_body, n_here);
         };
         float BX[16], BY[16];
-        chunk(nch - 1, BX);
         int ch = nch - 1;
-        for (; ch - 1 >= e0; ch -= 2) {
-          chunk_step(ch, BX, BY);
-          chunk_step(ch - 1, BY, BX);
+        if constexpr (KQV < 4) {
+          using QP = std::integral_constant<int, KQV>;
+          chunk_kq(QP{}, ch, BX);
+          chunk_step(QP{}, ch, BX, BY);
+          --ch;
+          for (; ch - 1 >= e0; ch -= 2) {
+            chunk_step(Q4{}, ch, BY, BX);
+            chunk_step(Q4{}, ch - 1, BX, BY);
+          }
+          if (ch >= e0) chunk_step(Q4{}, ch, BY, BX);
+        } else {
+          chunk(ch, BX);
+          for (; ch - 1 >= e0; ch -= 2) {
+            chunk_step(Q4{}, ch, BX, BY);
+            chunk_step(Q4{}, ch - 1, BY, BX);
+          }
+          if (ch >= e0) chunk_step(Q4{}, ch, BX, BY);
         }
-        if (ch >= e0) chunk_step(ch, BX, BY);
         if (e0 == 0) msave = mpart;
       }
       mpart = msave;
@@ -1054,7 +1092,16 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
 
 template <int DIM>
 hipError_t launch_c32(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
-  auto k = cm32_predict_kernel<DIM>;
+  // peeled when the last 64-row chunk has at least one all-padding k-quad (<= 48 live rows)
+  const int r_last = fa.n_train % 64;
+  int kqv = (r_last == 0 || getenv("BO_C32_NOPART") != nullptr) ? 4 : (r_last + 15) >> 4;
+  if (const char* f = getenv("BO_C32_KQV")) {   // A/B only: a larger count is still exact
+    const int v = atoi(f);
+    if (v > kqv && v <= 4) kqv = v;
+  }
+  auto k = kqv == 1 ? cm32_predict_kernel<DIM, 1>
+         : kqv == 2 ? cm32_predict_kernel<DIM, 2>
+         : kqv == 3 ? cm32_predict_kernel<DIM, 3> : cm32_predict_kernel<DIM, 4>;
   if (pl.lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)pl.lds);

@@ -14,7 +14,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "cpu_ref.c")
-LIB = os.path.join(HERE, "libcpu_ref.so")
+# BO_CPU_REF_LIB: another build of the same source (scripts/host_sanitize.sh's ASan/UBSan build)
+LIB = os.environ.get("BO_CPU_REF_LIB", os.path.join(HERE, "libcpu_ref.so"))
 # portable x86-64 (AVX2 + FMA): the GPU box's host CPU is not this container's
 FLAGS = ["-O3", "-march=x86-64-v3", "-fopenmp", "-shared", "-fPIC"]
 

@@ -10,6 +10,11 @@ reference's call) -> oracle/cpu_ref.c.  No K^-1 is shared between the two sides 
 config-size tests feed LAPACK's K^-1 to both).  Tolerances: SURVEY.md §8c (tests/parity.py);
 the top-q is judged tie-aware on the CPU acquisition array.
 
+Two inverse paths, each at every config: "cholesky" (what the device picks at these well-conditioned
+inputs) and "lu" (`lu_hint` forces every objective onto the blocked LU + getrs, bo_invert_k_ex --
+the path the drop-in loop actually takes at fitted length scales, DeviceBackend._lu_hint).  The
+oracle side is the same LAPACK gesv either way, so the two parametrisations share one CPU array.
+
 Configs (SURVEY.md §8d inputs): C3 (N = 512, the full 1024^2 'ij' grid, q = 3), C4 (N = 1024,
 the 2^21 unscrambled Sobol set, q = 3) and C5's shard 0 of 8 (N = 2048, 2^19 Sobol candidates,
 f64, q = 16).  The CPU arrays of C3 and C4 share tests/fullref.py's cache with
@@ -77,8 +82,9 @@ def _problem(bo, cfg):
     return x, y, 40.0, 16, cands, off, cnt, lambda: pts, ("C5chain", 0), excl
 
 
+@pytest.mark.parametrize("path", ["cholesky", "lu"])
 @pytest.mark.parametrize("cfg", ["C3", "C4", "C5shard0"])
-def test_device_chain_matches_oracle_chain(bo, cfg):
+def test_device_chain_matches_oracle_chain(bo, cfg, path):
     import torch
     x, y, ls_v, q, cands, off, cnt, host_pts, key, excl = _problem(bo, cfg)
     n, n_obj = x.shape[0], y.shape[1]
@@ -89,9 +95,12 @@ def test_device_chain_matches_oracle_chain(bo, cfg):
     km = torch.zeros((n_obj, n, n), dtype=torch.float64, device="cuda")
     bo.kernels.update_k(km, xd, 0, n, pv, ls)
     before = bo._lib.invert_k_path_counts()
-    kinv_dev = bo.kernels.invert_k(n, km)
+    taken = []
+    kinv_dev = bo.kernels.invert_k(n, km, lu_hint=[path == "lu"] * n_obj, paths=taken)
     after = bo._lib.invert_k_path_counts()
-    assert after["cholesky"] - before["cholesky"] == n_obj      # well-conditioned: Cholesky + Newton step
+    # well-conditioned: Cholesky + Newton step unless the hint sends every objective to the LU
+    assert after[path] - before[path] == n_obj, (before, after)
+    assert taken == [0 if path == "cholesky" else 1] * n_obj, taken
     r = bo.predict_acquire(xd, yd, kinv_dev, cands, pm, pv, ls, betas, outputs=("mu", "var", "acq"), topq=q,
                            offset=off, count=cnt)
     torch.cuda.synchronize()
@@ -110,5 +119,5 @@ def test_device_chain_matches_oracle_chain(bo, cfg):
         a = km_h[o] + 1e-6 * np.eye(n)
         res_got = np.abs(a @ kd[o] - np.eye(n)).max()
         res_ref = np.abs(a @ kinv_ref[o] - np.eye(n)).max()
-        print(f"{cfg} objective {o}: residual {res_got:.2e} (LAPACK {res_ref:.2e})")
+        print(f"{cfg} {path} objective {o}: residual {res_got:.2e} (LAPACK {res_ref:.2e})")
         assert res_got <= max(10.0 * res_ref, 1e-12), (o, res_got, res_ref)
