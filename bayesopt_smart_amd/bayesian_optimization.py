@@ -357,6 +357,8 @@ def optimize(x_vector, y_vector, kernel_matrices, k_star, mu_objectives, varianc
                 "acquisition_values": arrs["acquisition_values"],
                 "x_next": x_next,
                 "hyperparams": optimized.x,
+                # the reference's keys; update_k_star (its "kernels", :145-153) is fused into the
+                # predict call and so counted under "acquisition" here
                 "timings": {"hyperparams": t1 - t0, "kernels": t2 - t1, "acquisition": t3 - t2,
                             "eval": t4 - t3, "total": t4 - iter_start},
             })

@@ -381,6 +381,20 @@ struct KGen {
 #ifndef BO_SMALL_PF
 #define BO_SMALL_PF 2
 #endif
+// wait states of the upper form's completion fence (64: the MFMA's full latency; other values
+// only in diagnostic builds, BO_BUILD_VARIANT=DEF_FENCE_NOPS=<n>)
+#ifndef BO_FENCE_NOPS
+#define BO_FENCE_NOPS 64
+#endif
+// Diagnostic build (BO_BUILD_VARIANT=DEF_PREDICT_CLK, 2-D kernels): every wave of cm_tiles
+// records its shader-clock and 100 MHz real-time-clock spans; bo_debug_predict_clk reads them
+// back, so the core clock the kernel ran at is sum(clock) / sum(realtime) x 100 MHz.
+#if defined(BO_PREDICT_CLK) && defined(BO_PREDICT_DIM) && BO_PREDICT_DIM == 2
+#define BO_CLK_ON 1
+__device__ long long bo_predict_clk[2 * 4096];
+#else
+#define BO_CLK_ON 0
+#endif
 // PART (UPPER, N not a multiple of 32): the first chunk each group streams -- the last rows,
 // partly padding -- is peeled and its all-padding k-step pairs skip their MFMAs (their K* rows
 // are exactly 0, so the outputs are bit-identical) and, with the 4-deep ring, their W refills
@@ -425,6 +439,9 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #pragma unroll
   for (int k = 0; k < DIM; ++k) z[k] = SEP ? 0.0 : a.xpad[k];
 
+#if BO_CLK_ON
+  const long long clk0 = clock64(), rt0 = wall_clock64();
+#endif
   double top_v = -__builtin_inf();
   long long top_i = -1;
   double held_v = -__builtin_inf();     // a tile's candidates waiting for the paired insert
@@ -520,11 +537,22 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         // all kCMaxEp accumulator pairs zeroed unconditionally (zeroing only the group's eN
         // pairs behind nested guards measured 1-2 % slower at C2/C3/C4; starting them instead
         // with the inline constant 0 as C in a peeled first chunk: C2/C3 unchanged, C4 +1.2 %)
+#ifndef BO_ABL_NOZERO
 #pragma unroll
         for (int e = 0; e < MAXEP; ++e) {
           acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
           acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
         }
+#else
+        // ablation: the accumulators are not zeroed (wrong results; timing only)
+        if (tile == t_first && o == 0 && e0 == 0) {
+#pragma unroll
+          for (int e = 0; e < MAXEP; ++e) {
+            acc[e][0] = (d4){0.0, 0.0, 0.0, 0.0};
+            acc[e][1] = (d4){0.0, 0.0, 0.0, 0.0};
+          }
+        }
+#endif
         // one chunk: MFMAs from register set B while the next chunk's K* is generated into Bn
         // in three stages inside E-pair 0's MFMA stream (the sets alternate: no register
         // copies between the chunks), and mu += alpha . B.  Branch-free: the last chunk
@@ -568,7 +596,13 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             // 822 ms at 4.7 TB of fetches; a runtime switch around the barrier cost 1 % in both
             // settings.  Kept for every explicit / Sobol kernel.
             if constexpr (!SEP) __builtin_amdgcn_s_barrier();
+#ifdef BO_ABL_NOGEN
+            // ablation: no next-chunk generation and no mean (every chunk reuses the first
+            // chunk's K*; wrong results, timing only)
+            if constexpr (false) {
+#else
             if constexpr (e == 0) {
+#endif
               gen.s0(K, al, ch, chn, g, An);
               __builtin_amdgcn_sched_barrier(0);
             }
@@ -592,7 +626,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               (void)so;   // ablation: the primed W values are reused (no W traffic; timing only)
 #endif
               ++pos;
+#ifdef BO_ABL_NOGEN
+              if constexpr (false) {
+#else
               if constexpr (e == 0) {
+#endif
                 if (pp == 0) {
                   __builtin_amdgcn_sched_barrier(0);
                   gen.s1(K, Bn);
@@ -618,7 +656,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             if constexpr (UPPER) {
 #endif
               if (ch - e0 == e) {
-                mfma_fence<BO_ACC_AGPR, 64>(acc[e][0], acc[e][1]);
+                mfma_fence<BO_ACC_AGPR, BO_FENCE_NOPS>(acc[e][0], acc[e][1]);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   qpart = __builtin_fma(B[r], acc[e][0][r], qpart);
@@ -632,6 +670,10 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
         const int c0 = upper ? nch - 1 : 0;
         double BX[8], BY[8];
         K.chunk(c0, g, BX);
+#ifdef BO_ABL_NOGEN
+#pragma unroll
+        for (int s = 0; s < 8; ++s) BY[s] = BX[s];
+#endif
         int ch = c0;
         if constexpr (PART && UPPER) {
           const int r_last = a.n_train - 32 * (nch - 1);
@@ -769,6 +811,16 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   }
   if (held) bo_wave_topq_insert16(top_v, top_i, held_v, held_i, a.topq);
   BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
+#if BO_CLK_ON
+  {
+    const long long clk1 = clock64(), rt1 = wall_clock64();
+    const int wid = blockIdx.x * kWaves + wave;
+    if (lane == 0 && wid < 4096) {
+      bo_predict_clk[2 * wid] = clk1 - clk0;
+      bo_predict_clk[2 * wid + 1] = rt1 - rt0;
+    }
+  }
+#endif
   if (a.topq > 0) {
     if (lane < a.topq) {
       TopEntry* dst = a.partial + ((size_t)blockIdx.x * kWaves + wave) * a.topq;
@@ -1099,9 +1151,12 @@ hipError_t launch_c32(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
     const int v = atoi(f);
     if (v > kqv && v <= 4) kqv = v;
   }
+  // two live k-quads run the 3-quad kernel: the KQV = 2 instantiation measured slower than it
+  // (C5 at N = 2064 / 2080, the same problem forced onto each: KQV 1 407.5, 2 427.4, 3 423.3,
+  // 4 431.6 ms, profiles/r06_c5_fp32_kqv_probe.txt) -- its code, not its MFMA count, which is
+  // lower; every peeled kernel is exact for any larger count of live k-quads
   auto k = kqv == 1 ? cm32_predict_kernel<DIM, 1>
-         : kqv == 2 ? cm32_predict_kernel<DIM, 2>
-         : kqv == 3 ? cm32_predict_kernel<DIM, 3> : cm32_predict_kernel<DIM, 4>;
+         : kqv <= 3 ? cm32_predict_kernel<DIM, 3> : cm32_predict_kernel<DIM, 4>;
   if (pl.lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)pl.lds);
@@ -1128,6 +1183,16 @@ hipError_t BO_CAT(launch_cms_d, BO_PREDICT_SMALL_DIM)(const Plan& pl, const Fuse
                 : launch_cm_k<D, false, false, false, 4>(fa, pl.grid, pl.lds, st);
 }
 }  // namespace bo
+#endif
+#if BO_CLK_ON
+// diagnostic build only: the per-wave (shader clock, 100 MHz clock) spans of the last 2-D
+// launch (2 words per wave, `n` waves at most); returns the waves copied
+extern "C" __attribute__((visibility("default"))) int bo_debug_predict_clk(long long* out, int n) {
+  if (n > 4096) n = 4096;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bo_predict_clk), sizeof(long long) * 2 * n) != hipSuccess) return -1;
+  return n;
+}
 #endif
 #ifdef BO_PREDICT_DIM
 namespace bo {

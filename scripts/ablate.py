@@ -40,7 +40,7 @@ print(json.dumps({{'lib': os.path.basename({lib!r}), 'cfg': {cfg!r}, 'mode': {mo
 
 
 if __name__ == "__main__":
-    libs = [a for a in sys.argv[1:] if a.endswith(".so")]
+    libs = [os.path.abspath(a) for a in sys.argv[1:] if a.endswith(".so")]   # dlopen needs a path
     modes = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("mode=")] or ["auto"]
     cfgs = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("cfg=")] or ["C3"]
     for rnd in range(2):
