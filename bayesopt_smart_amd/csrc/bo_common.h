@@ -34,6 +34,17 @@ __device__ __forceinline__ bool bo_bound(bool ok, const char* what, long long v,
 #endif
 
 // MIN_VARIANCE / KERNEL_JITTER / CHOLESKY_JITTER: bayesopt/config.py:57-66 (fp64 branch).
+// Wait states between an MFMA writing its accumulators and their first VALU / v_accvgpr_read,
+// supplied INSIDE the fences' asm statements (hipcc pads after an asm statement only by its own
+// estimate, which under-counted gfx950's f64 MFMA in round 1).  One wait state is
+// one s_nop issue slot, 4 clocks (MI355X guide: `s_nop 0` costs 4 cycles).  gfx950 runs
+// v_mfma_f64_16x16x4_f64 in 16 passes (64 clocks, measured): the dependent read needs passes + 4
+// = 20 states, given 24 here; v_mfma_f32_16x16x4_f32 is 8 passes (12 states), given 16.  Rounds
+// 1-5 used 64 states (256 clocks), the MFMA's latency counted in clocks: that padding cost 2.6 %
+// of the C3 kernel (32 fences per 64-candidate tile; profiles/r06_c3_ablation.jsonl).
+#define BO_NOPS_F64_MFMA "s_nop 7\n\ts_nop 7\n\ts_nop 7"
+#define BO_NOPS_F32_MFMA "s_nop 7\n\ts_nop 7"
+
 #define BO_MIN_VARIANCE 1e-10
 #define BO_MIN_VARIANCE_F32 1e-6    // the float32 branch's floor (config.py:57-61), BO_PREDICT_F32_FLOOR
 #define BO_KERNEL_JITTER 1e-6

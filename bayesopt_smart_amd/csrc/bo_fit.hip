@@ -628,10 +628,10 @@ __global__ __launch_bounds__(256) void inv_extract_kernel(double* __restrict__ o
   }
 }
 
-// 64 wait states between the last MFMA writing the accumulators and their first VALU read (the
-// round-1 gfx950 hazard)
+// the f64 MFMA's read wait states (BO_NOPS_F64_MFMA, bo_common.h) between the last MFMA writing
+// the accumulators and their first VALU read (the round-1 gfx950 hazard)
 __device__ __forceinline__ void mfma_fence_acc(d4 (&acc)[2][2]) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+  asm volatile(BO_NOPS_F64_MFMA
                : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]));
 }
 

@@ -313,7 +313,7 @@ __device__ __forceinline__ void r16_finish(const double* __restrict__ A, long lo
 
 // an f64 MFMA's result is read by plain VALU / LDS instructions only after its latency: wait states
 __device__ __forceinline__ void acc_fence(d4& x) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(x));
+  asm volatile(BO_NOPS_F64_MFMA : "+v"(x));         // bo_common.h
 }
 
 // Step s applied to a strip whose rows [16 s, n_p) are in registers (base = 16 s): the

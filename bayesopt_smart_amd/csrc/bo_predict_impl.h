@@ -199,24 +199,23 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 // another block (observed: stale rows of the last MFMA, deterministic data-dependent errors
 // up to 0.15 pv).  The asm consumes and "redefines" both accumulators in place, so it cannot be
 // scheduled before the MFMAs that produce them and no read of them can be hoisted above it;
-// its 64 wait states cover the MFMA's full latency.
+// its wait states (BO_NOPS_F64_MFMA, bo_common.h) cover the MFMA's latency.
 // (bo_predict_s<D>.hip keeps the accumulators in arch VGPRs: the fence's operand constraint follows)
 #ifdef BO_PREDICT_SMALL_DIM
 #define BO_ACC_AGPR false
 #else
 #define BO_ACC_AGPR true
 #endif
-template <bool AGPR, int NOPS = 64>
+// NOPS: 0 = ordering only (ablation builds), else the f64 MFMA's read wait states (bo_common.h)
+template <bool AGPR, int NOPS = 1>
 __device__ __forceinline__ void mfma_fence(d4& x, d4& y) {
-#define BO_NOPS8 "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
   if (NOPS == 0) {
     if (AGPR) asm volatile("" : "+a"(x), "+a"(y));
     else asm volatile("" : "+v"(x), "+v"(y));
   } else {
-    if (AGPR) asm volatile(BO_NOPS8 : "+a"(x), "+a"(y));
-    else asm volatile(BO_NOPS8 : "+v"(x), "+v"(y));
+    if (AGPR) asm volatile(BO_NOPS_F64_MFMA : "+a"(x), "+a"(y));
+    else asm volatile(BO_NOPS_F64_MFMA : "+v"(x), "+v"(y));
   }
-#undef BO_NOPS8
 }
 
 // vmcnt(n) with expcnt / lgkmcnt left at their maxima (gfx9 s_waitcnt encoding)
@@ -381,10 +380,10 @@ struct KGen {
 #ifndef BO_SMALL_PF
 #define BO_SMALL_PF 2
 #endif
-// wait states of the upper form's completion fence (64: the MFMA's full latency; other values
-// only in diagnostic builds, BO_BUILD_VARIANT=DEF_FENCE_NOPS=<n>)
+// the upper form's completion fence: 1 = BO_NOPS_F64_MFMA (bo_common.h); 0 (ordering only, no
+// wait states) only in diagnostic builds, BO_BUILD_VARIANT=DEF_FENCE_NOPS=0
 #ifndef BO_FENCE_NOPS
-#define BO_FENCE_NOPS 64
+#define BO_FENCE_NOPS 1
 #endif
 // Diagnostic build (BO_BUILD_VARIANT=DEF_PREDICT_CLK, 2-D kernels): every wave of cm_tiles
 // records its shader-clock and 100 MHz real-time-clock spans; bo_debug_predict_clk reads them
@@ -507,6 +506,14 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
       for (int k = 0; k < DIM; ++k) c[k] -= z[k];
     }
     double acq = 0.0;
+#ifndef BO_RING_RESET
+    // W ring: primed once per tile and running on across the objectives: the objectives' streams
+    // lie back to back, so the last refills of objective o load objective o + 1's first pairs
+    // (past the last objective they read beyond the stream: zeros or the next pairs, never used)
+    d2 wa[PF], wb[PF];
+    prime_ring(wr, voff, 0, wa, wb);
+    int pos = 0;
+#endif
     for (int o = 0; o < a.n_obj; ++o) {
       if (SEP && !a.rw_cache) row_pass(c, o, o + 1);
       KRows<DIM, SEP> K;
@@ -520,13 +527,18 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #pragma unroll
       for (int k = 0; k < DIM; ++k) K.c[k] = c[k];
       const double* al = alpha + (size_t)o * a.n_pad;
-      // W ring: primed per objective (a ring running on across objectives and tiles, wrapping
-      // at the end of the packed streams, measured 1.7 % slower at C4 and 3 % faster at C2 on
-      // one box: its modular refill offsets defeat the immediate-offset addressing)
+#ifdef BO_RING_RESET
+      // (A/B build: the ring primed per objective.  A ring running on across the TILES too,
+      // wrapping at the end of the packed streams, measured 1.7 % slower at C4 and 3 % faster at
+      // C2 in round 2: its modular refill offsets defeat the immediate-offset addressing)
       const int base = o * w_obj;
       d2 wa[PF], wb[PF];
       prime_ring(wr, voff, base, wa, wb);
       int pos = 0;
+#else
+      constexpr int base = 0;
+      (void)w_obj;
+#endif
       double mpart = 0.0, qpart = 0.0, msave = 0.0;
       d4 acc[MAXEP][2];
       // E-pairs in groups of kCMaxEp (the accumulators one wave holds: 512 rows); a group
@@ -716,7 +728,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               const int cur = e & 1, nxt = cur ^ 1;
               const bool more = e + 1 < eN;
               if (more) gq[nxt].s0k(K, e0 + e + 1, g);
-              mfma_fence<BO_ACC_AGPR, 64>(acc[e][0], acc[e][1]);
+              mfma_fence<BO_ACC_AGPR>(acc[e][0], acc[e][1]);
               if (more) gq[nxt].s1(K, S[nxt]);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
@@ -935,7 +947,7 @@ __device__ __forceinline__ f4 wload32(__amdgpu_buffer_rsrc_t r, int voff, int so
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 __device__ __forceinline__ void mfma_fence32(f4& a, f4& b, f4& c, f4& d) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+  asm volatile(BO_NOPS_F32_MFMA
                : "+a"(a), "+a"(b), "+a"(c), "+a"(d));
 }
 
@@ -990,6 +1002,13 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
 #pragma unroll
     for (int k = 0; k < DIM; ++k) c32[k] = (float)(c[k] - z[k]);
     double acq = 0.0;
+#ifndef BO_RING_RESET
+    // the W ring runs on across the objectives (their streams lie back to back), as in cm_tiles
+    f4 w[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[q] = wload32(wr, voff, q * 1024);
+    int pos = 0;
+#endif
     for (int o = 0; o < a.n_obj; ++o) {
       const float nl2 = (float)(a.nhl[o] * 1.4426950408889634);
       const float lpv = (float)log2(a.pv[o]);
@@ -1010,11 +1029,16 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
       using Q4 = std::integral_constant<int, 4>;
       auto chunk = [&](int ch, float (&B)[16]) { chunk_kq(Q4{}, ch, B); };
       const float* alo = al + (size_t)o * a.n_pad;
+#ifdef BO_RING_RESET
       const int base = (int)(o * w_obj);
       f4 w[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) w[q] = wload32(wr, voff, base + q * 1024);
       int pos = 0;
+#else
+      constexpr int base = 0;
+      (void)w_obj;
+#endif
       float mpart = 0.0f, qpart = 0.0f, msave = 0.0f;
       f4 acc[kC32MaxEp][4];
       for (int e0 = 0; e0 < nch; e0 += kC32MaxEp) {
