@@ -1,6 +1,6 @@
 #!/bin/bash
 # The round's evidence set with the shipped library, in phases that each fit one gpurun call:
-#   bash scripts/gpu_evidence.sh TAG tests|bench|pmc1|pmc2|iter
+#   bash scripts/gpu_evidence.sh TAG tests|bench|pmc1|pmc2|iter|c5cpu|c5cpu64
 # Outputs under gpurun_out/TAG/ (copied into profiles/ afterwards).  Every GPU step runs under
 # its own time limit; the first failing step ends the phase.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -67,5 +67,10 @@ case $PHASE in
     step iter_c5 500 python bench.py --iteration --config C5
     pmc fit $B --fit --config C3
     stats fit $B --fit --config C3 ;;
+  c5cpu)      # C5 (fp32, the config's stated precision) with cpu_baseline and the whole set scored on
+              # the host cores for selection_matches_cpu (--cpu-full: 4,194,304 candidates at N = 2048)
+    step bench_c5_cpufull 1100 python -u bench.py --config C5 --steps 3 --warmup 2 --cpu-full ;;
+  c5cpu64)
+    step bench_c5f64_cpufull 1100 python -u bench.py --config C5 --mode auto --steps 3 --warmup 2 --cpu-full ;;
   *) echo "unknown phase $PHASE"; exit 2 ;;
 esac

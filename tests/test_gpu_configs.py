@@ -210,3 +210,61 @@ def test_sharded_predict_acquire_device_path_single_rank(bo):
     np.testing.assert_array_equal(gi, ref["top_idx"].cpu().numpy())
     np.testing.assert_array_equal(out["acq"].cpu().numpy(), ref["acq"].cpu().numpy())
     assert r["acq"].data_ptr() == out["acq"].data_ptr()
+
+
+def test_replay_after_workspace_growth(bo):
+    """The round-2 fault hypothesis: a prepared call or HIP graph that kept
+    only the workspace POINTER, replayed after a larger call grew (re-allocated) the per-stream
+    workspace and the old storage was handed out again, would write into freed memory.  Since
+    round 3 the prepared call owns its workspace tensor.  Here: a graph and a prepared call are
+    captured on a small problem; a call with q = 48 on a larger problem (the failing round-2
+    test's q) grows the workspace; the freed storage is then refilled with garbage by fresh
+    allocations; both replays must still reproduce the direct call bit for bit, and the
+    workspace cache must now hold a different (larger) buffer."""
+    import torch
+    from bayesopt_smart_amd.device import Workspace
+    rng = np.random.default_rng(5)
+    side, n = 128, 64
+    lin = rng.choice(side * side, size=n, replace=False)
+    x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+    y = toy_function(x)
+    pm, pv = y.mean(0), y.var(0)
+    ls, betas = np.array([9.0, 13.0]), np.array([2.0, 2.0])
+    km = np.zeros((2, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    kinv = O.invert_k(n, km)
+    xd, yd, kd = (torch.tensor(a, device="cuda") for a in (x, y, kinv))
+    cands = bo.CandidateSet.grid([(0, side), (0, side)])
+    args = (xd, yd, kd, cands, pm, pv, ls, betas)
+    torch.cuda.synchronize()
+    Workspace._cache.clear()          # start from a small workspace (earlier tests grew the shared one)
+    ref = bo.predict_acquire(*args, outputs=("mu", "var", "acq"), topq=3)
+    ref = {k: ref[k].cpu().numpy() for k in ("mu", "var", "acq", "top_idx")}
+    prep = bo.predict_acquire(*args, outputs=("mu", "var", "acq"), topq=3, prepare=True)
+    graph = bo.predict_acquire(*args, outputs=("mu", "var", "acq"), topq=3, prepare=True).graphed()
+    torch.cuda.synchronize()
+    ws_before = {k: v.data_ptr() for k, v in Workspace._cache.items()}
+    # a much larger call on the same stream: N = 1024, the 1024^2 grid, q = 48
+    side2, n2 = 1024, 1024
+    lin2 = rng.choice(side2 * side2, size=n2, replace=False)
+    x2 = np.stack([lin2 // side2, lin2 % side2], axis=1).astype(np.float64)
+    y2 = toy_function(x2)
+    pm2, pv2 = y2.mean(0), y2.var(0)
+    km2 = np.zeros((2, n2, n2))
+    O.update_k(km2, x2, 0, n2, pv2, ls * 4)
+    kinv2 = O.invert_k(n2, km2)
+    big = bo.predict_acquire(x2, y2, kinv2, bo.CandidateSet.grid([(0, side2), (0, side2)]), pm2, pv2, ls * 4,
+                             betas, outputs=("acq",), topq=48)
+    torch.cuda.synchronize()
+    assert big["top_idx"].cpu().numpy().min() >= 0
+    grown = [k for k, v in Workspace._cache.items() if k in ws_before and v.data_ptr() != ws_before[k]]
+    assert grown, "the large call did not grow the workspace (the test would prove nothing)"
+    # hand the freed storage out again and scribble over it
+    junk = [torch.full((1 << 20,), float("nan"), dtype=torch.float64, device="cuda") for _ in range(64)]
+    torch.cuda.synchronize()
+    for run in (prep, graph):
+        res = run()
+        torch.cuda.synchronize()
+        for k in ("mu", "var", "acq", "top_idx"):
+            np.testing.assert_array_equal(res[k].cpu().numpy(), ref[k], err_msg=k)
+    del junk
