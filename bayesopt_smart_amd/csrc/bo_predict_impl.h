@@ -650,11 +650,24 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
                 } else if (pp == 2) {
                   __builtin_amdgcn_sched_barrier(0);
                   gen.s2(K, chn, g, Bn);
+#ifdef BO_GEN_PIN
+                  // A/B only (BO_BUILD_VARIANT=DEF_GEN_PIN): LLVM sinks s2 and the mean out of this
+                  // body into the chunk's exit block, past the sched barriers (their values are
+                  // next read after the chunk).  Pinning them here with an IR-level use measured
+                  // slower everywhere, outputs bit-identical (round 6, same box: C3 8.32 -> 8.37,
+                  // C4 108.4 -> 116.2, C5-fp32 394 -> 406, C5-f64 813 -> 867 ms;
+                  // profiles/r06_gen_pin_ab.jsonl): the sunk placement stays
+                  asm volatile("" : "+v"(Bn[0]), "+v"(Bn[1]), "+v"(Bn[2]), "+v"(Bn[3]), "+v"(Bn[4]),
+                               "+v"(Bn[5]), "+v"(Bn[6]), "+v"(Bn[7]));
+#endif
                   __builtin_amdgcn_sched_barrier(0);
                 } else if (pp == 3) {
                   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                   for (int s = 0; s < 8; ++s) mpart = __builtin_fma(An[s], B[s], mpart);
+#ifdef BO_GEN_PIN
+                  asm volatile("" : "+v"(mpart));
+#endif
                   __builtin_amdgcn_sched_barrier(0);
                 }
               }
@@ -1074,6 +1087,12 @@ __global__ __launch_bounds__(256, 1) void cm32_predict_kernel(const FusedArgs a)
                 mpart = __builtin_fmaf(av, B[s], mpart);   // group 0's is kept (msave)
               }
               chunk(chn, Bn);
+#ifdef BO_GEN_PIN
+              // (A/B only, as in cm_tiles: pinning the generation here measured slower)
+              asm volatile("" : "+v"(Bn[0]), "+v"(Bn[1]), "+v"(Bn[2]), "+v"(Bn[3]), "+v"(Bn[4]), "+v"(Bn[5]),
+                           "+v"(Bn[6]), "+v"(Bn[7]), "+v"(Bn[8]), "+v"(Bn[9]), "+v"(Bn[10]), "+v"(Bn[11]),
+                           "+v"(Bn[12]), "+v"(Bn[13]), "+v"(Bn[14]), "+v"(Bn[15]), "+v"(mpart));
+#endif
             }
 #pragma unroll
             for (int kq = 0; kq < kqv; ++kq) {
