@@ -399,6 +399,13 @@ __device__ long long bo_predict_clk[2 * 4096];
 // are exactly 0, so the outputs are bit-identical) and, with the 4-deep ring, their W refills
 // (one instantiation per count of live pairs: the refills issued anyway cost N = 518 2 %).  A separate instantiation: the multiples
 // of 32 keep the loop's code layout (peeling it into the one kernel cost C3 1.5 %, C4 3 %).
+// the sched barriers that place the next chunk's generation stages between E-pair 0's MFMA
+// pairs (BO_BUILD_VARIANT=DEF_NO_SCHED_PIN drops them: A/B only)
+#ifdef BO_NO_SCHED_PIN
+#define BO_GEN_SB ((void)0)
+#else
+#define BO_GEN_SB __builtin_amdgcn_sched_barrier(0)
+#endif
 template <int DIM, bool SEP, bool UPPER, bool GROWS, int MAXEP, bool PART = false>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   constexpr bool upper = UPPER;
@@ -616,7 +623,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
             if constexpr (e == 0) {
 #endif
               gen.s0(K, al, ch, chn, g, An);
-              __builtin_amdgcn_sched_barrier(0);
+              BO_GEN_SB;
             }
 #pragma unroll
             for (int pp = 0; pp < 4; ++pp) {
@@ -644,11 +651,11 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
               if constexpr (e == 0) {
 #endif
                 if (pp == 0) {
-                  __builtin_amdgcn_sched_barrier(0);
+                  BO_GEN_SB;
                   gen.s1(K, Bn);
-                  __builtin_amdgcn_sched_barrier(0);
+                  BO_GEN_SB;
                 } else if (pp == 2) {
-                  __builtin_amdgcn_sched_barrier(0);
+                  BO_GEN_SB;
                   gen.s2(K, chn, g, Bn);
 #ifdef BO_GEN_PIN
                   // A/B only (BO_BUILD_VARIANT=DEF_GEN_PIN): LLVM sinks s2 and the mean out of this
@@ -660,15 +667,15 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
                   asm volatile("" : "+v"(Bn[0]), "+v"(Bn[1]), "+v"(Bn[2]), "+v"(Bn[3]), "+v"(Bn[4]),
                                "+v"(Bn[5]), "+v"(Bn[6]), "+v"(Bn[7]));
 #endif
-                  __builtin_amdgcn_sched_barrier(0);
+                  BO_GEN_SB;
                 } else if (pp == 3) {
-                  __builtin_amdgcn_sched_barrier(0);
+                  BO_GEN_SB;
 #pragma unroll
                   for (int s = 0; s < 8; ++s) mpart = __builtin_fma(An[s], B[s], mpart);
 #ifdef BO_GEN_PIN
                   asm volatile("" : "+v"(mpart));
 #endif
-                  __builtin_amdgcn_sched_barrier(0);
+                  BO_GEN_SB;
                 }
               }
             }

@@ -22,6 +22,7 @@ import bench  # noqa: E402
 args = dict(a.split("=", 1) for a in sys.argv[1:] if "=" in a)
 cfg_name = args.get("cfg", "C3")
 reps = int(args.get("reps", 5))
+idle_ms = float(args.get("idle_ms", 0))          # host idle before each timed launch (DVFS ramp)
 cfg = bench.CONFIGS[cfg_name]
 x, y, pm, pv, ls, betas, kinv, cand = bench.make_config_problem(cfg, 1)
 c = bo.CandidateSet.grid([(0, cand[1]), (0, cand[2])]) if cand[0] == "grid" else cand[1]
@@ -36,9 +37,12 @@ n = x.shape[0]
 m = cand[1] * cand[2] if cand[0] == "grid" else c.n
 mfma_flops = bench.executed_mfma_flops_per_candidate("upper", n, len(pm)) * m
 mfma_per_simd = mfma_flops / 2048 / 1024                    # 256 CUs x 4 SIMDs
+import time  # noqa: E402
 for r in range(reps + 2):
     call()
     torch.cuda.synchronize()
+    if idle_ms > 0:
+        time.sleep(idle_ms / 1000.0)
     L.bo_profile_start(1)
     call()
     torch.cuda.synchronize()
@@ -53,7 +57,7 @@ for r in range(reps + 2):
     f_ghz = spans[:, 0].sum() / spans[:, 1].sum() * 0.1
     rt_ms = spans[:, 1] / 1e5
     mfma_ms = mfma_per_simd * 64 / (f_ghz * 1e9) * 1e3
-    print(f"{cfg_name}: kernel {ms.value:.3f} ms; waves {len(spans)}; core clock {f_ghz:.3f} GHz "
+    print(f"{cfg_name} (idle {idle_ms:g} ms before): kernel {ms.value:.3f} ms; waves {len(spans)}; core clock {f_ghz:.3f} GHz "
           f"(per-wave min {spans[:, 0].min() / spans[:, 1].max() * 0.1:.3f}); wave span {rt_ms.min():.3f} .. "
           f"{rt_ms.max():.3f} ms; MFMA-bound time at that clock {mfma_ms:.3f} ms "
           f"({mfma_ms / ms.value:.3f} of the kernel), at 2.4 GHz {mfma_per_simd * 64 / 2.4e9 * 1e3:.3f} ms",
