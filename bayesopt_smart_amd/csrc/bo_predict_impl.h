@@ -406,7 +406,17 @@ __device__ long long bo_predict_clk[2 * 4096];
 #else
 #define BO_GEN_SB __builtin_amdgcn_sched_barrier(0)
 #endif
-template <int DIM, bool SEP, bool UPPER, bool GROWS, int MAXEP, bool PART = false>
+// LANEQ (1 <= q <= 4, the integer-grid SEP path): every lane keeps its own top-4 of the candidates
+// it scores (lane group 0; order keys), inserted only when a candidate beats the lane's q-th entry
+// and is not an evaluated point; the wave's list is formed once, at the end (one 64-entry sort).
+// The general path shares one wave list and tests every tile against its q-th entry by readlanes
+// (SGPR spills to VGPR lanes: 199 -> 86 in the C2 kernel without it); with the top-q compiled out
+// C2 ran 5 % faster (0.2195 -> 0.2073 ms, C3 -0.3 %, C4 -0.6 %).  Same box, outputs bit-identical
+// (profiles/r06_topq_ab.jsonl): C2 0.2205 -> 0.2136 ms, C3 unchanged; on the Sobol path (C4) the
+// lanes' lower thresholds send more candidates through the exclusion's hash probe in global
+// memory: 108.1 -> 111.2 ms, so the explicit / Sobol kernels keep the wave list.
+constexpr int kLaneQ = 4;
+template <int DIM, bool SEP, bool UPPER, bool GROWS, int MAXEP, bool PART = false, bool LANEQ = false>
 __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
   constexpr bool upper = UPPER;
   // W ring depth in pairs of k-steps: kPF, or BO_SMALL_PF = 2 for the small-N kernels (their W
@@ -450,6 +460,10 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 #endif
   double top_v = -__builtin_inf();
   long long top_i = -1;
+  unsigned long long lk[kLaneQ];        // LANEQ: the lane's list (order keys, selection order)
+  long long lx[kLaneQ];
+#pragma unroll
+  for (int t = 0; t < kLaneQ; ++t) { lk[t] = 0ull; lx[t] = -1; }
   double held_v = -__builtin_inf();     // a tile's candidates waiting for the paired insert
   long long held_i = -1;
   bool held = false;
@@ -794,12 +808,22 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
     if (a.topq > 0) {
 #endif
       // exclusion of evaluated points (acquisition.py:137-139: all coordinates equal), tested
-      // only when a candidate would enter the wave's list
+      // only when a candidate would enter the wave's list (LANEQ: the lane's list)
       const long long gi0 = valid ? a.cand_offset + j : -1;
-      double tv;
-      long long ti;
-      bo_wave_topq_threshold(top_v, top_i, a.topq, tv, ti);
-      const bool need = gi0 >= 0 && bo_better(acq, gi0, tv, ti);
+      bool need;
+      unsigned long long kc = 0ull;
+      if constexpr (LANEQ) {
+        kc = bo_order_key(acq, gi0);
+        const int q = a.topq;
+        const unsigned long long kq = q == 1 ? lk[0] : q == 2 ? lk[1] : q == 3 ? lk[2] : lk[3];
+        const long long xq = q == 1 ? lx[0] : q == 2 ? lx[1] : q == 3 ? lx[2] : lx[3];
+        need = g == 0 && gi0 >= 0 && bo_key_before(kc, gi0, kq, xq);
+      } else {
+        double tv;
+        long long ti;
+        bo_wave_topq_threshold(top_v, top_i, a.topq, tv, ti);
+        need = gi0 >= 0 && bo_better(acq, gi0, tv, ti);
+      }
       bool hit = false;
       if (__ballot(need) != 0ull) {
         if (SEP && !a.excl && a.rw_cache) {
@@ -826,6 +850,22 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
           hit = valid && bo_hash_contains(a.hkeys, a.hidx, a.hmask, a.excl ? a.excl : a.xpad, DIM, co, DIM);
         }
       }
+      if constexpr (LANEQ) {
+        // (group 0's lane holds this candidate's own exclusion result)
+        if (need && !hit) {
+          // sorted insertion: entries the new one beats move down one slot
+#pragma unroll
+          for (int t = kLaneQ - 1; t >= 0; --t) {
+            const bool before_t = bo_key_before(kc, gi0, lk[t], lx[t]);
+            const bool after_prev = t == 0 || !bo_key_before(kc, gi0, lk[t > 0 ? t - 1 : 0], lx[t > 0 ? t - 1 : 0]);
+            if (before_t) {
+              lk[t] = after_prev ? kc : lk[t > 0 ? t - 1 : 0];
+              lx[t] = after_prev ? gi0 : lx[t > 0 ? t - 1 : 0];
+            }
+          }
+        }
+        continue;
+      }
       const unsigned long long hb = __ballot(hit);
       const bool excluded =
           ((hb >> jl) | (hb >> (jl + 16)) | (hb >> (jl + 32)) | (hb >> (jl + 48))) & 1ull;
@@ -842,6 +882,23 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
     }
   }
   if (held) bo_wave_topq_insert16(top_v, top_i, held_v, held_i, a.topq);
+  if constexpr (LANEQ) {
+    // the wave's list from the 16 lanes' lists: entry t of group-0 lane jl goes to lane jl + 16 t,
+    // then one 64-entry sort in selection order (lanes 0 .. q-1 are written below)
+    const int src = lane & 15, t = lane >> 4;
+    unsigned long long kk = 0ull;
+    long long xx = -1;
+#pragma unroll
+    for (int u = 0; u < kLaneQ; ++u) {
+      const unsigned long long ku = __shfl(lk[u], src, 64);
+      const long long xu = __shfl(lx[u], src, 64);
+      kk = t == u ? ku : kk;
+      xx = t == u ? xu : xx;
+    }
+    top_v = bo_key_value(kk);
+    top_i = kk == 0ull ? -1 : xx;
+    bo_wave_sort64(top_v, top_i);
+  }
   BO_WAIT_VMCNT(0);                                          // no W load in flight at exit
 #if BO_CLK_ON
   {
@@ -870,7 +927,7 @@ __device__ __forceinline__ void cm_tiles(const FusedArgs& a, double* smem) {
 // (W ring priming, first-chunk generation, accumulator fences, the epilogue's divisions and
 // square roots, the top-q shuffles) are long against the tile's 160 MFMAs, and the second
 // wave on each SIMD issues its MFMAs while the first waits in them.
-template <int DIM, bool GRID, bool UPPER, bool GROWS, int MAXEP, bool PART = false>
+template <int DIM, bool GRID, bool UPPER, bool GROWS, int MAXEP, bool PART = false, bool LANEQ = false>
 __global__ __launch_bounds__(256, MAXEP <= 4 ? 2 : 1) void cm_predict_kernel(const FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int tid = threadIdx.x;
@@ -895,14 +952,14 @@ __global__ __launch_bounds__(256, MAXEP <= 4 ? 2 : 1) void cm_predict_kernel(con
   }
   __syncthreads();
   if constexpr (GRID && !GROWS) {
-    if (sep) { cm_tiles<DIM, true, UPPER, false, MAXEP, PART>(a, smem); return; }
+    if (sep) { cm_tiles<DIM, true, UPPER, false, MAXEP, PART, LANEQ>(a, smem); return; }
   }
-  cm_tiles<DIM, false, UPPER, GROWS, MAXEP, PART>(a, smem);
+  cm_tiles<DIM, false, UPPER, GROWS, MAXEP, PART>(a, smem);   // (the lane lists: SEP only)
 }
 
-template <int DIM, bool GRID, bool UPPER, bool GROWS, int MAXEP, bool PART = false>
+template <int DIM, bool GRID, bool UPPER, bool GROWS, int MAXEP, bool PART = false, bool LANEQ = false>
 hipError_t launch_cm_k(const FusedArgs& fa, int grid, size_t lds, hipStream_t st) {
-  auto k = cm_predict_kernel<DIM, GRID, UPPER, GROWS, MAXEP, PART>;
+  auto k = cm_predict_kernel<DIM, GRID, UPPER, GROWS, MAXEP, PART, LANEQ>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
@@ -910,6 +967,12 @@ hipError_t launch_cm_k(const FusedArgs& fa, int grid, size_t lds, hipStream_t st
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, fa);
   return hipGetLastError();
+}
+
+// the lane-local top-q (cm_tiles LANEQ) for 1 <= q <= 4; BO_TOPQ_WAVE=1 keeps the wave list (A/B)
+inline bool lane_topq(const FusedArgs& fa) {
+  static const bool off = getenv("BO_TOPQ_WAVE") != nullptr;
+  return !off && fa.topq >= 1 && fa.topq <= kLaneQ;
 }
 
 template <int DIM, bool UPPER, bool GROWS>
@@ -922,11 +985,15 @@ hipError_t launch_cm_u(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
     else return bo::launch_cms_d8(pl, fa, st);
   }
   if constexpr (UPPER) {
+    const bool laneq = lane_topq(fa);
     // a partly padded last chunk (the drop-in loop's N) with at least one all-padding k-step
     // pair; with 25..31 rows (nothing to skip) the peeled layout measured +1.4 %
-    if (fa.n_train % 32 != 0 && fa.n_train % 32 <= 24)
+    if (fa.n_train % 32 != 0 && fa.n_train % 32 <= 24) {
+      if (laneq && pl.sep) return launch_cm_k<DIM, true, true, false, bo::kCMaxEp, true, true>(fa, pl.grid, pl.lds, st);
       return pl.sep ? launch_cm_k<DIM, true, true, false, bo::kCMaxEp, true>(fa, pl.grid, pl.lds, st)
                     : launch_cm_k<DIM, false, true, false, bo::kCMaxEp, true>(fa, pl.grid, pl.lds, st);
+    }
+    if (laneq && pl.sep) return launch_cm_k<DIM, true, true, false, bo::kCMaxEp, false, true>(fa, pl.grid, pl.lds, st);
   }
   return pl.sep ? launch_cm_k<DIM, true, UPPER, false, bo::kCMaxEp>(fa, pl.grid, pl.lds, st)
                 : launch_cm_k<DIM, false, UPPER, false, bo::kCMaxEp>(fa, pl.grid, pl.lds, st);
@@ -1226,6 +1293,7 @@ hipError_t launch_c32(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
 namespace bo {
 hipError_t BO_CAT(launch_cms_d, BO_PREDICT_SMALL_DIM)(const Plan& pl, const FusedArgs& fa, hipStream_t st) {
   constexpr int D = BO_PREDICT_SMALL_DIM;
+  if (fa.upper && pl.sep && lane_topq(fa)) return launch_cm_k<D, true, true, false, 4, false, true>(fa, pl.grid, pl.lds, st);
   if (fa.upper)
     return pl.sep ? launch_cm_k<D, true, true, false, 4>(fa, pl.grid, pl.lds, st)
                   : launch_cm_k<D, false, true, false, 4>(fa, pl.grid, pl.lds, st);
