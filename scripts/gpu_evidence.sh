@@ -1,6 +1,6 @@
 #!/bin/bash
 # The round's evidence set with the shipped library, in phases that each fit one gpurun call:
-#   bash scripts/gpu_evidence.sh TAG tests|bench|pmc1|pmc2|iter|c5cpu|c5cpu64
+#   bash scripts/gpu_evidence.sh TAG tests|bench|pmc1|pmc2|iter|c5cpu|c5cpu64|dist
 # Outputs under gpurun_out/TAG/ (copied into profiles/ afterwards).  Every GPU step runs under
 # its own time limit; the first failing step ends the phase.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -72,5 +72,8 @@ case $PHASE in
     step bench_c5_cpufull 1100 python -u bench.py --config C5 --steps 3 --warmup 2 --cpu-full ;;
   c5cpu64)
     step bench_c5f64_cpufull 1100 python -u bench.py --config C5 --mode auto --steps 3 --warmup 2 --cpu-full ;;
+  dist)       # bench.py's multi-rank step rehearsed on one device (gloo, P = 1, 2, 4), C2 C3 C4 C5
+    CFGS="C2 C3 C4 C5" step dist_rehearsal 1100 bash scripts/gpu_dist_rehearsal.sh
+    cp gpurun_out/dist/rehearsal.jsonl "$OUT/dist_rehearsal.jsonl" ;;
   *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
