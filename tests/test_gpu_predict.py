@@ -246,3 +246,39 @@ def test_predict_grid_row_factor_paths(bo, shape, n, n_obj, offset):
     shard_pts = np.stack(np.unravel_index(offset + np.arange(count), shape), axis=1)
     excl = _excluded(shard_pts, x)
     check_topq(out["top_idx"] - offset, out["acq"], excl, 8)
+
+
+@pytest.mark.parametrize("q", [1, 2, 3, 4, 5])
+def test_grid_topq_exclusion_at_the_top(bo, q):
+    """The fused kernel's top-q on the separable integer-grid path, where q <= 4 uses the lanes'
+    own lists (cm_tiles LANEQ) and q = 5 the wave-shared list: with beta = 0 the acquisition is
+    the standardised mean, which here peaks at the best training points, so the evaluated points
+    (acquisition.py:137-139, excluded through the grid row's bitmap) lead the order.  The selection must be exactly the order of the call's own acquisition
+    array over the non-evaluated candidates (descending, ties by index)."""
+    import torch
+    rng = np.random.default_rng(21 + q)
+    side, n = 256, 40
+    lin = rng.choice(side * side, size=n, replace=False)
+    x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+    # a few high training points and short length scales: the mean peaks AT them
+    y = np.zeros((n, 2))
+    y[:6, 0] = [1000, 900, 800, 700, 600, 500]
+    y[:6, 1] = [50, 40, 30, 20, 10, 5]
+    y[6:] = rng.normal(size=(n - 6, 2))
+    pm, pv = y.mean(0), y.var(0)
+    ls, betas = np.array([3.0, 3.0]), np.zeros(2)
+    km = np.zeros((2, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    kinv = O.invert_k(n, km)
+    cands = bo.CandidateSet.grid([(0, side), (0, side)])
+    r = bo.predict_acquire(x, y, kinv, cands, pm, pv, ls, betas, outputs=("acq",), topq=q)
+    torch.cuda.synchronize()
+    acq = r["acq"].cpu().numpy()
+    excl = np.zeros(side * side, dtype=bool)
+    excl[lin] = True
+    order_all = np.lexsort((np.arange(side * side), -acq))
+    assert excl[order_all[:q]].any(), "no evaluated point at the top: the case is not exercised"
+    a = np.where(excl, -np.inf, acq)
+    want = np.lexsort((np.arange(side * side), -a))[:q]
+    np.testing.assert_array_equal(r["top_idx"].cpu().numpy(), want)
+    np.testing.assert_array_equal(r["top_val"].cpu().numpy(), acq[want])
