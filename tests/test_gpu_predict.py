@@ -282,3 +282,32 @@ def test_grid_topq_exclusion_at_the_top(bo, q):
     want = np.lexsort((np.arange(side * side), -a))[:q]
     np.testing.assert_array_equal(r["top_idx"].cpu().numpy(), want)
     np.testing.assert_array_equal(r["top_val"].cpu().numpy(), acq[want])
+
+
+@pytest.mark.parametrize("n", [518, 530, 541])
+def test_grid_part_lane_topq_vs_cpu(bo, n):
+    """The drop-in loop's own kernel shape on the integer grid: N off a multiple of 32 (the PART
+    instantiation, 1 / 3 / 3 live k-step pairs in the peeled chunk: N = 518 / 530 / 541) with
+    q = 3 (the lane-local top-q lists), every candidate of a 512 x 1024 'ij' grid against the CPU
+    reference (oracle/cpu_ref.c, SURVEY.md §8c tolerances) and the top-3 judged on the CPU
+    acquisition array."""
+    import torch
+    rng = np.random.default_rng(n)
+    rows, side = 512, 1024
+    lin = rng.choice(rows * side, size=n, replace=False)
+    x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+    y = np.stack([-((x[:, 0] - 150) ** 2) + 100, -((x[:, 1] - 150) ** 2) + 20], axis=1)
+    pm, pv = y.mean(0), y.var(0)
+    ls, betas = np.array([20.0, 20.0]), np.array([2.0, 2.0])
+    km = np.zeros((2, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    kinv = O.invert_k(n, km)
+    cands = bo.CandidateSet.grid([(0, rows), (0, side)])
+    r = bo.predict_acquire(x, y, kinv, cands, pm, pv, ls, betas, outputs=("mu", "var", "acq"), topq=3)
+    torch.cuda.synchronize()
+    got = {k: r[k].cpu().numpy() for k in ("mu", "var", "acq", "top_idx")}
+    ref = cpu_full(("grid_part", n), x, y, grid_points_2d(rows, side), kinv, pm, pv, ls, betas)
+    check_predict({k: got[k] for k in ("mu", "var", "acq")}, ref, pv)
+    excl = np.zeros(rows * side, dtype=bool)
+    excl[lin] = True
+    check_topq(got["top_idx"], ref["acq"], excl, 3)
