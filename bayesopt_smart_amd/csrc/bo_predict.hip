@@ -572,7 +572,13 @@ int make_plan(const bo_predict_desc* d, Plan* pl, bool query_device, bool kmem =
   const long long n_tiles = (d->n_cand + kTile - 1) / kTile;
   pl->n_tiles = n_tiles;
   const int cus = query_device ? num_cus() : 256;
+#ifdef BO_SMALL_ONE_SLOT
+  // diagnostic build (BO_BUILD_VARIANT=DEF_SMALL_ONE_SLOT): the small kernel on one workgroup per
+  // CU, i.e. one wave per SIMD -- what a two-tile wave would run at
+  const int slots = cus;
+#else
   const int slots = pl->small ? 2 * cus : cus;
+#endif
   pl->grid = (int)(n_tiles < slots ? (n_tiles > 0 ? n_tiles : 1) : slots);
   pl->off_alpha = align256(w_bytes);
   pl->off_xpad = pl->off_alpha + align256((size_t)d->n_obj * n_pad * sizeof(double));
