@@ -14,7 +14,7 @@ shapes:
     PART peel, 1..3 live k-step pairs) and multiples of 32, up to the GROWS layout (rows and alpha
     in global memory, N = 1600 on the grid and 2100 on a 6-D set);
   * q = 1..4 (the lane-local top-q lists on the SEP path), 5, 7, 8 and 16 (the wave-shared list);
-  * n_obj 1..4; shards with a non-zero offset and a count that is not a multiple of the 64-
+  * n_obj 1..8 (BO_MAX_OBJ); shards with a non-zero offset and a count that is not a multiple of the 64-
     candidate tile;
   * modes: auto (upper form), dense, auto-exp (no separable generation), and fp32 (the f32 kernel,
     cm32_predict_kernel<DIM, KQV>: every KQV -- last 64-row chunk with 1, 3 or 4 live k-quads).
@@ -74,6 +74,11 @@ CASES = [
     ("fp32-sobol4-n700-kqv4-q4", "sobol", 4, 700, 3, 4, "fp32", 0, None),
     ("fp32-sobol8-n1200-kqv3-q2", "sobol", 8, 1200, 1, 2, "fp32", 0, None),
     ("fp32-grid-n150-q3", "grid", (128, 96), 150, 2, 3, "fp32", 0, None),
+    # more objectives than the BASELINE configs (BO_MAX_OBJ = 8)
+    ("grid-nobj8-n200-q3", "grid", (256, 256), 200, 8, 3, "auto", 0, None),
+    ("grid-nobj5-n100-small-q2", "grid", (128, 256), 100, 5, 2, "auto", 0, None),
+    ("sobol6-nobj6-n300-q5", "sobol", 6, 300, 6, 5, "auto", 0, None),
+    ("fp32-sobol6-nobj5-n600-q4", "sobol", 6, 600, 5, 4, "fp32", 0, None),
 ]
 
 
