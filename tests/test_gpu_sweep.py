@@ -264,3 +264,44 @@ def test_kernel_variant_vs_cpu(bo, case):
     da = np.abs(got["acq"] - ref["acq"])
     assert (da <= tol).all(), (cid, int((da > tol).sum()), float(np.max(da / tol)))
     check_topq(got["top_idx"] - off, ref["acq"], excl, q, tol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("count", [0, 1, 15, 17, 63, 65])
+@pytest.mark.parametrize("q", [1, 3, 5])
+def test_tiny_grid_shards(bo, count, q):
+    """Shards smaller than one wave's 16 candidates or one 64-candidate tile, on the separable grid
+    path (lane-local top-q for q <= 4): every candidate against the CPU reference, the selection
+    in the reference's order over the shard (evaluated points skipped), -1 past the shard's
+    selectable candidates."""
+    import torch
+    from oracle import cpu_ref
+    rng = np.random.default_rng(1000 + 10 * count + q)
+    side, n = 256, 60
+    off = 16 * 300
+    lin = rng.choice(side * side - 1, size=n, replace=False)
+    lin[lin >= off] += 1                               # distinct from off
+    if count:
+        lin[0] = off                                   # an evaluated point inside the shard
+    x = np.stack([lin // side, lin % side], axis=1).astype(np.float64)
+    y = rng.normal(size=(n, 2)) * 20
+    pm, pv = y.mean(0), y.var(0)
+    ls, betas = np.array([9.0, 11.0]), np.array([1.0, 2.0])
+    km = np.zeros((2, n, n))
+    O.update_k(km, x, 0, n, pv, ls)
+    kinv = O.invert_k(n, km)
+    cs = bo.CandidateSet.grid([(0, side), (0, side)])
+    r = bo.predict_acquire(x, y, kinv, cs, pm, pv, ls, betas, outputs=("mu", "var", "acq"), topq=q,
+                           offset=off, count=count)
+    torch.cuda.synchronize()
+    got = {k: r[k].cpu().numpy() for k in ("mu", "var", "acq", "top_idx", "top_val")}
+    idx = np.arange(off, off + count)
+    if count:
+        pts = np.stack([idx // side, idx % side], axis=1).astype(np.float64)
+        ref = cpu_ref.predict_acquire(x, y, pts, kinv, pm, pv, ls, betas)
+        check_predict({k: got[k] for k in ("mu", "var", "acq")}, ref, pv)
+    excl = np.isin(idx, lin)
+    a = np.where(excl, -np.inf, got["acq"])
+    want = idx[np.lexsort((idx, -a))][: min(q, int((~excl).sum()))]
+    np.testing.assert_array_equal(got["top_idx"][: want.size], want)
+    assert (got["top_idx"][want.size:] == -1).all()
