@@ -265,17 +265,44 @@ def _lib_sha256():
         return hashlib.sha256(fh.read()).hexdigest()
 
 
+def device_code_sha256(path):
+    """sha256 of a library's device code: the bytes of its .hip_fatbin ELF section (every gfx950
+    code object the kernels run from).  A relink of the same objects -- or a rebuild of the same
+    sources at the same path -- leaves it unchanged where the file's own sha256 may differ in host
+    bytes; None if the section is missing."""
+    import hashlib
+    import struct
+    with open(path, "rb") as fh:
+        data = fh.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2:                       # ELF64 only
+        return None
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    sec = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stro = sec[shstrndx][4]
+    for name, _typ, _fl, _addr, off, size, *_ in sec:
+        end = data.index(b"\0", stro + name)
+        if data[stro + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()
+    return None
+
+
 def pmc_traffic(workload="C3"):
     """HBM bytes per fused-kernel launch from a committed rocprofv3 PMC summary of this workload
-    (profiles/*pmc*.json, scripts/pmc_summary.py) taken with THIS libbo_amd.so (its lib_sha256);
-    None when no summary of this binary exists (a summary of another build is never used)."""
+    (profiles/*pmc*.json, scripts/pmc_summary.py) taken with THIS library's kernels: its file
+    sha256 (lib_sha256), or the sha256 of its device code (fatbin_sha256, device_code_sha256) --
+    the counters count the kernels, and a relink that changes only host bytes keeps them.  None
+    when no summary of these kernels exists (a summary of another build is never used)."""
+    from bayesopt_smart_amd import _lib
     sha = _lib_sha256()
+    fsha = device_code_sha256(_lib.LIB_PATH)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
     for f in reversed(files):
         try:
             with open(f) as fh:
                 d = json.load(fh)
-            if d.get("workload") == workload and d.get("hbm_bytes_per_launch") and d.get("lib_sha256") == sha:
+            same = d.get("lib_sha256") == sha or (fsha is not None and d.get("fatbin_sha256") == fsha)
+            if d.get("workload") == workload and d.get("hbm_bytes_per_launch") and same:
                 return float(d["hbm_bytes_per_launch"]), os.path.basename(f)
         except Exception:
             pass

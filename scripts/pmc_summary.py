@@ -36,7 +36,10 @@ def main(src, dst, workload="C3", alg_bytes=40 * 1048576, kernel_label="cm_predi
                                                      "bayesopt_smart_amd", "libbo_amd.so"))
     with open(lib, "rb") as fh:
         lib_sha = hashlib.sha256(fh.read()).hexdigest()
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import device_code_sha256
     out = {"workload": workload, "kernel": kernel_label, "lib_sha256": lib_sha,
+           "fatbin_sha256": device_code_sha256(lib),
            "counters_per_launch": mean, "launches_per_counter": {k: len(v) for k, v in vals.items()}}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         fetch = 2.0 * mean["FETCH_SIZE"] * 1024.0       # gfx950 16-B-read correction

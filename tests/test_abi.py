@@ -88,3 +88,31 @@ def test_workspace_size_queries():
     d.topq, d.n_obj = 3, 9
     assert lib.bo_predict_workspace_size(d) == 0          # over BO_MAX_OBJ
     assert lib.bo_select_topq_workspace_size(1000, 3) > 0
+
+
+def test_device_code_sha_identifies_the_kernels(tmp_path):
+    """bench.py's PMC matching key: the sha256 of the library's .hip_fatbin section (every gfx950
+    code object).  It exists for the in-tree library, it is the section llvm-objcopy dumps, and a
+    file without that section (here: the library's host part only) has none."""
+    import shutil
+    import subprocess
+    import sys
+    sys.path.insert(0, ROOT)
+    import hashlib
+    from bench import device_code_sha256
+    from bayesopt_smart_amd import _lib
+    sha = device_code_sha256(_lib.LIB_PATH)
+    assert sha is not None and re.fullmatch(r"[0-9a-f]{64}", sha)
+    objcopy = "/opt/rocm/llvm/bin/llvm-objcopy"
+    if os.path.exists(objcopy):
+        dump = tmp_path / "fatbin.bin"
+        subprocess.run([objcopy, f"--dump-section=.hip_fatbin={dump}", _lib.LIB_PATH, str(tmp_path / "x.so")],
+                       check=True, capture_output=True)
+        assert hashlib.sha256(dump.read_bytes()).hexdigest() == sha
+        host = tmp_path / "host.so"
+        subprocess.run([objcopy, "--remove-section=.hip_fatbin", _lib.LIB_PATH, str(host)], check=True,
+                       capture_output=True)
+        assert device_code_sha256(str(host)) is None
+    not_elf = tmp_path / "not_elf.bin"
+    shutil.copyfile(os.path.join(ROOT, "README.md"), not_elf)
+    assert device_code_sha256(str(not_elf)) is None
